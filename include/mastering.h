@@ -1,0 +1,162 @@
+/*
+ * mastering.h — C-ABI of the MI355X mastering engine (libmastering_amd.so).
+ *
+ * Drop-in boundary for the reference's hot path
+ *   worker/audio_mastering_engine.py:24  process_audio_from_gcs(gcs_uri, settings)
+ * whose per-chunk DSP is AME:48-77 (saturation AME:128, EQ AME:146, width AME:136,
+ * int16 quantise AME:123, multiband AME:196) and whose whole-track tail is
+ * AME:80-89 (concat, LUFS normalise AME:212, soft limiter AME:224, int16).
+ * The Python host (python-audio-mastering_amd/mastering_amd/engine.py) mirrors the
+ * reference's `process(...)`/`apply_*` surface and calls these entry points via
+ * ctypes.  Plain pointers and sizes only; no torch types.
+ *
+ * Conventions: every function returns 0 on success and a negative code on error;
+ * mm_last_error() then holds a message (per context, NUL terminated).  One context
+ * per host thread; a context owns one hipStream_t and its device work buffers.
+ * Host-side filter design (EQ/crossover/K-weighting coefficients, compressor
+ * max-attenuation tables, state-transition powers, chunk and loudness-block
+ * geometry) is done by the caller in f64 with the reference's exact expressions
+ * and passed in mm_job, so coefficients are bit-identical to the reference's.
+ */
+#ifndef MASTERING_AMD_H
+#define MASTERING_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MM_OK 0
+#define MM_ERR_ARG (-1)
+#define MM_ERR_HIP (-2)
+#define MM_ERR_RCCL (-3)
+#define MM_ERR_STATE (-4)
+
+#define MM_MAX_DIM 8      /* max IIR state dimension per channel (4 biquads) */
+#define MM_SCAN_POWERS 12 /* powers Phi^(c*2^k), k < MM_SCAN_POWERS */
+
+#define MM_OUT_I16 0 /* interleaved int16 PCM (what AME:89/98 writes)            */
+#define MM_OUT_F32 1 /* interleaved f32 = the same PCM / 32768 (decoded form)    */
+
+typedef struct mm_ctx mm_ctx;
+
+/* One IIR stage = 1..2 branches of cascaded DF2T biquads fed by the same input.
+ * sos[s] = {b0, b1, b2, a1, a2} (a0 == 1), branches laid out branch-major.
+ * phi/phi_pow/phi_last: state-transition matrices (row-major MM_MAX_DIM x
+ * MM_MAX_DIM, only dim x dim used) of the zero-input recurrence over one tile
+ * (phi), over c*2^k tiles (phi_pow[k], c = tiles per scan thread) and over the
+ * last (possibly partial) tile of a line (phi_last). */
+typedef struct mm_iir {
+    int32_t nsec;            /* total sections (0 = stage inactive)           */
+    int32_t nsec_branch0;    /* sections in branch 0 (rest are branch 1)      */
+    int32_t dim;             /* state dim per channel = 2 * nsec              */
+    int32_t scan_c;          /* tiles per scan thread the powers were made for */
+    double sos[4][5];
+    double phi[MM_MAX_DIM * MM_MAX_DIM];
+    double phi_pow[MM_SCAN_POWERS][MM_MAX_DIM * MM_MAX_DIM];
+    double phi_last[MM_MAX_DIM * MM_MAX_DIM];
+} mm_iir;
+
+/* Per-band pydub compress_dynamic_range parameters (AME:207-209). */
+typedef struct mm_band {
+    double thresh_rms;       /* 32768 * 10**(thr/20)                          */
+    double attack_frames;    /* attack_ms * (rate/1000.0)                      */
+    double release_frames;   /* release_ms * (rate/1000.0)                     */
+    int32_t look;            /* int(attack_frames)                             */
+    int32_t _pad;
+    const double *max_att;   /* host table [32769]: max attenuation for rms r  */
+} mm_band;
+
+/* A mastering job for one track (geometry + settings, all host memory). */
+typedef struct mm_job {
+    int64_t frames_in;       /* decoded input frames N                         */
+    int64_t frames_proc;     /* processed frames (pydub 30 s slicing, AME:48-54) */
+    int32_t channels;        /* 1 or 2                                         */
+    int32_t rate;
+    int32_t tile;            /* frames per tile T (divides every full chunk)    */
+    int32_t tiles_per_chunk; /* K = chunk_frames / T                            */
+    /* settings (AME:58-86) */
+    float sat_keep;          /* f32(1 - mix)      (AME:131-134), mix=(s/100)^2 */
+    float sat_mix;           /* f32(mix)                                        */
+    float sat_drive;         /* f32(1 + 4*mix)                                  */
+    int32_t sat_on;          /* saturation != 0                                 */
+    double width;            /* AME:60-61                                       */
+    int32_t width_on;        /* width != 1.0 and stereo                         */
+    int32_t multiband_on;    /* AME:65                                          */
+    int32_t lufs_on;         /* settings["lufs"] is not None (AME:84)           */
+    int32_t out_kind;        /* MM_OUT_I16 | MM_OUT_F32                         */
+    double lufs_target;
+    mm_iir eq;               /* AME:154-161, active stages only                */
+    mm_iir xover;            /* butter(4) LP250 (branch 0) + HP4000 (branch 1)  */
+    mm_iir kweight;          /* pyloudnorm high_shelf then high_pass            */
+    mm_band band[3];         /* low / mid / high                                */
+    int32_t comp_warmup;     /* speculative warm-up frames per tile             */
+    int32_t comp_max_iters;  /* cap on fix-up sweeps (exactness check)          */
+    /* loudness geometry (pyloudnorm integrated_loudness, block 0.4 s, step 0.1 s) */
+    int64_t n_blocks;
+    const int64_t *block_lo; /* host [n_blocks] first frame of each block        */
+    const int64_t *block_hi; /* host [n_blocks] one-past-last frame (clamped)    */
+    int64_t n_segs;          /* distinct boundaries - 1                         */
+    const int64_t *seg_bounds; /* host [n_segs+1] sorted distinct block bounds   */
+    double block_scale;      /* 1.0 / (0.4 * rate)                              */
+} mm_job;
+
+typedef struct mm_result {
+    double loudness;         /* integrated loudness of the pre-gain mix (LUFS)   */
+    double gain_linear;      /* 10 ** ((target - L) / 20), 1.0 if lufs off       */
+    int64_t frames_out;      /* == frames_proc                                   */
+    int32_t comp_iters;      /* fix-up sweeps the compressor needed              */
+    int32_t _pad;
+} mm_result;
+
+/* ---- context ------------------------------------------------------------ */
+int mm_create(int device, mm_ctx **ctx);
+int mm_destroy(mm_ctx *ctx);
+const char *mm_last_error(mm_ctx *ctx);
+int mm_sync(mm_ctx *ctx);
+int mm_version(void);
+
+/* ---- whole chain -------------------------------------------------------- */
+/* Host buffers: in = interleaved f32 [frames_in*channels] (PCM16/32768),
+ * out = [frames_proc*channels] of out_kind.  Replaces AME:43-98 minus file/GCS IO. */
+int mm_master(mm_ctx *ctx, const mm_job *job, const float *in, void *out, mm_result *res);
+/* Same, with device-resident input/output (zero-copy; e.g. torch tensors). */
+int mm_master_device(mm_ctx *ctx, const mm_job *job, const float *d_in, void *d_out, mm_result *res);
+
+/* ---- staged entry points (time-sharded multi-GPU, parity probes) -------- */
+/* Run AME:48-80 for this job's chunks into the context's int16 mix buffer and
+ * the K-weighting per-tile aggregates (state carry-in assumed 0). */
+int mm_stage_chunks(mm_ctx *ctx, const mm_job *job, const float *d_in);
+/* K-weighting end state of this job's range from a zero start: dim doubles. */
+int mm_kweight_range_end(mm_ctx *ctx, double *end_state_host);
+/* Per-segment K-weighted energies given a carry-in state (host [dim] or NULL);
+ * writes n_segs doubles to host. */
+int mm_hop_energies(mm_ctx *ctx, const double *carry_in_host, double *seg_energy_host);
+/* Gated loudness from full-track segment energies (host, C restatement of
+ * pyloudnorm's gating); returns L via *loudness. */
+int mm_gate_loudness(const mm_job *job, const double *seg_energy, double *loudness);
+/* Apply gain + soft limiter + quantise (AME:84-89) to the staged mix. */
+int mm_finalize(mm_ctx *ctx, double gain_linear, int use_gain, void *d_out);
+/* Copy the staged pre-gain int16 mix (interleaved) to host (parity probe). */
+int mm_read_mix(mm_ctx *ctx, int16_t *host_mix);
+
+/* ---- timing (HIP events on the context stream) -------------------------- */
+/* Enable per-kernel event timing; stats are averages over launches. */
+int mm_timing(mm_ctx *ctx, int enable);
+/* names: '\n'-joined kernel names into buf; ms/launches arrays of cap entries. */
+int mm_kernel_stats(mm_ctx *ctx, char *names, int names_cap, double *total_ms, int64_t *launches, int cap);
+
+/* ---- RCCL over xGMI ----------------------------------------------------- */
+int mm_comm_unique_id(char id_out[128]);
+int mm_comm_init(mm_ctx *ctx, int rank, int nranks, const char id[128]);
+int mm_comm_destroy(mm_ctx *ctx);
+/* In-place sum all-reduce of n doubles in host memory (staged through HBM). */
+int mm_allreduce_sum_f64(mm_ctx *ctx, double *host_buf, int64_t n);
+/* All-gather of n doubles per rank: out = [nranks * n]. */
+int mm_allgather_f64(mm_ctx *ctx, const double *host_in, double *host_out, int64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,296 @@
+"""TEST INFRASTRUCTURE ONLY — CPU oracle of the reference mastering chain.
+
+Only `tests/`, `__graft_entry__.smoke()` and `bench.py`'s `cpu_baseline` leg may
+import this module, and only as the checker / the timed CPU baseline.  The
+product path (python-audio-mastering_amd/) never imports it.
+
+It restates `worker/audio_mastering_engine.py` ("AME") of the reference,
+vectorised with numpy/scipy, with the third-party pieces (pydub compressor,
+pyloudnorm meter) restated per oracle/thirdparty_restated.py.  The compressor
+loop itself runs in C (oracle/compressor_oracle.c, built by oracle/Makefile).
+
+Pinning: tests/golden/make_golden.py runs the reference's OWN code (stub-imported
+with the restated third-party modules) on short synthetic clips and commits the
+inputs/outputs under tests/golden/; tests/test_oracle.py checks this module
+against those vectors bit for bit.  The pydub/pyloudnorm boundary itself is
+"parity unpinned" (the reference has no tests that hold a fixture for it).
+
+dtype flow (numpy 2.x, NEP 50 — the versions in this image):
+  int16 -> f32 /32768 (AME:117-121) -> saturation f32 (AME:128-134)
+  -> EQ: each active stage is a 1-section sosfilt, f64 out (AME:146-194)
+  -> width in the EQ's dtype (AME:136-144) -> clip, *32768, astype(int16) (AME:123-126)
+  -> multiband: int16/32768 f32 -> butter(4) LP250/HP4000 sosfilt f64,
+     mid = x-lo-hi, 3x quantise, 3x compress, overlay (AME:196-210)
+  -> concat (AME:80) -> f32 (AME:82) -> LUFS: mono mean f32, K-weight lfilter
+     stored back to f32, gated loudness; gain is np.float64 so the product is
+     f64 (AME:212-222) -> soft limiter (AME:224-227) -> int16 (AME:89).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import scipy.signal
+
+from . import thirdparty_restated as tp
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "build", "libcompressor_oracle.so")
+
+EQ_PRESETS = {  # AME:15-20 (values; descriptions omitted)
+    "techno": {"bass_boost": 4.0, "mid_cut": 3.0, "presence_boost": 1.0, "treble_boost": 3.0},
+    "dubstep": {"bass_boost": 5.0, "mid_cut": 4.0, "presence_boost": 2.0, "treble_boost": 3.5},
+    "pop": {"bass_boost": 2.0, "mid_cut": 0.0, "presence_boost": 3.5, "treble_boost": 2.5},
+    "rock": {"bass_boost": 1.5, "mid_cut": -2.0, "presence_boost": 2.5, "treble_boost": 1.0},
+}
+
+
+# ----------------------------------------------------------------------------
+# C compressor loop
+# ----------------------------------------------------------------------------
+def build():
+    src = os.path.join(_HERE, "compressor_oracle.c")
+    if os.path.exists(_LIB) and os.path.getmtime(_LIB) >= os.path.getmtime(src):
+        return _LIB
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+    return _LIB
+
+
+_lib = None
+
+
+def _clib():
+    global _lib
+    if _lib is None:
+        _lib = ctypes.CDLL(build())
+        i16p = ctypes.POINTER(ctypes.c_int16)
+        d = ctypes.c_double
+        _lib.oracle_compress_band.argtypes = [i16p, i16p, ctypes.c_int64, ctypes.c_int, d, d, d, d, d,
+                                              ctypes.POINTER(ctypes.c_double)]
+        _lib.oracle_compress_trace.argtypes = [i16p, ctypes.c_int64, ctypes.c_int, d, d, d, d, d, d,
+                                               ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(ctypes.c_double)]
+    return _lib
+
+
+def compress_band(x: np.ndarray, rate: int, threshold: float, ratio: float, attack: float, release: float,
+                  return_att: bool = False):
+    """pydub compress_dynamic_range on an int16 array [F] or [F, ch]."""
+    x = np.ascontiguousarray(x, dtype=np.int16)
+    ch = 1 if x.ndim == 1 else x.shape[1]
+    frames = x.shape[0]
+    out = np.empty_like(x)
+    att = np.empty(frames, np.float64) if return_att else None
+    i16p = ctypes.POINTER(ctypes.c_int16)
+    _clib().oracle_compress_band(x.ctypes.data_as(i16p), out.ctypes.data_as(i16p), frames, ch,
+                                 float(threshold), float(ratio), float(attack), float(release), float(rate),
+                                 att.ctypes.data_as(ctypes.POINTER(ctypes.c_double)) if return_att else None)
+    return (out, att) if return_att else out
+
+
+def compress_trace(x, rate, threshold, ratio, attack, release, att0, start, stop):
+    x = np.ascontiguousarray(x, dtype=np.int16)
+    ch = 1 if x.ndim == 1 else x.shape[1]
+    out = np.empty(stop - start, np.float64)
+    _clib().oracle_compress_trace(x.ctypes.data_as(ctypes.POINTER(ctypes.c_int16)), x.shape[0], ch,
+                                  float(threshold), float(ratio), float(attack), float(release), float(rate),
+                                  float(att0), start, stop, out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    return out
+
+
+# ----------------------------------------------------------------------------
+# pointwise stages
+# ----------------------------------------------------------------------------
+def pcm_to_float(q: np.ndarray) -> np.ndarray:
+    return q.astype(np.float32) / 32768  # AME:121 (sample_width 2)
+
+
+def quantize(x: np.ndarray) -> np.ndarray:
+    return (np.clip(x, -1.0, 1.0) * 32768).astype(np.int16)  # AME:124-125
+
+
+def saturation(x: np.ndarray, percent) -> np.ndarray:
+    if percent == 0:  # AME:129
+        return x
+    m = (percent / 100.0) ** 2
+    return (1 - m) * x + m * np.tanh(x * (1 + m * 4))
+
+
+def stereo_width(x: np.ndarray, w) -> np.ndarray:
+    if x.ndim == 1 or x.shape[1] != 2:
+        return x
+    l, r = x[:, 0], x[:, 1]
+    mid = (l + r) / 2
+    side = (l - r) / 2
+    side = side * w
+    return np.array([mid + side, mid - side]).T
+
+
+def soft_limiter(x: np.ndarray, thr=0.98) -> np.ndarray:
+    x = x.copy()
+    a = np.abs(x)
+    k = a > thr
+    d = a[k] - thr
+    x[k] = (thr + d / (1 + (d / 0.02) ** 2) ** 0.5) * np.sign(x[k])
+    return x
+
+
+# ----------------------------------------------------------------------------
+# filter design (AME:170-194, AME:197-198)
+# ----------------------------------------------------------------------------
+def shelf_sos(rate, fc, gain_db, kind, q=0.707):
+    Wn = fc / (0.5 * rate)
+    g = 10.0 ** (gain_db / 20.0)
+    c = np.cos(Wn * 2 * np.pi)
+    al = np.sin(Wn * 2 * np.pi) / (2.0 * q)
+    sg = np.sqrt(g)
+    if kind == "low":
+        b = (g * ((g + 1) - (g - 1) * c + 2 * sg * al), 2 * g * ((g - 1) - (g + 1) * c),
+             g * ((g + 1) - (g - 1) * c - 2 * sg * al))
+        a = ((g + 1) + (g - 1) * c + 2 * sg * al, -2 * ((g - 1) + (g + 1) * c), (g + 1) + (g - 1) * c - 2 * sg * al)
+    else:
+        b = (g * ((g + 1) + (g - 1) * c + 2 * sg * al), -2 * g * ((g - 1) + (g + 1) * c),
+             g * ((g + 1) + (g - 1) * c - 2 * sg * al))
+        a = ((g + 1) - (g - 1) * c + 2 * sg * al, 2 * ((g - 1) - (g + 1) * c), (g + 1) - (g - 1) * c - 2 * sg * al)
+    return np.array([[b[0] / a[0], b[1] / a[0], b[2] / a[0], 1, a[1] / a[0], a[2] / a[0]]])
+
+
+def peak_sos(rate, fc, gain_db, q=1.0):
+    Wn = fc / (0.5 * rate)
+    g = 10.0 ** (gain_db / 20.0)
+    al = np.sin(Wn * 2 * np.pi) / (2.0 * q)
+    c2 = -2 * np.cos(Wn * 2 * np.pi)
+    b0, b1, b2 = 1 + al * g, c2, 1 - al * g
+    a0, a1, a2 = 1 + al / g, c2, 1 - al / g
+    return np.array([[b0 / a0, b1 / a0, b2 / a0, 1, a1 / a0, a2 / a0]])
+
+
+def eq_stages(rate, settings):
+    """Active EQ stages in AME order (AME:154-161); a 0 dB stage is skipped (AME:171,186)."""
+    bass = settings.get("bass_boost", 0.0)
+    mid = settings.get("mid_cut", 0.0)
+    pres = settings.get("presence_boost", 0.0)
+    treb = settings.get("treble_boost", 0.0)
+    st = []
+    if bass != 0:
+        st.append(shelf_sos(rate, 250, bass, "low"))
+    if -mid != 0:
+        st.append(peak_sos(rate, 1000, -mid))
+    if pres != 0:
+        st.append(peak_sos(rate, 4000, pres))
+    if treb != 0:
+        st.append(shelf_sos(rate, 8000, treb, "high"))
+    return st
+
+
+def equalize(x: np.ndarray, rate, settings) -> np.ndarray:
+    stages = eq_stages(rate, settings)
+    if x.ndim > 1 and x.shape[1] == 2:
+        chans = [x[:, 0], x[:, 1]]
+        for sos in stages:
+            chans = [scipy.signal.sosfilt(sos, c) for c in chans]
+        return np.array(chans).T
+    for sos in stages:
+        x = scipy.signal.sosfilt(sos, x)
+    return x
+
+
+def crossover_sos(rate, lo=250, hi=4000):
+    return (scipy.signal.butter(4, lo, btype="lowpass", fs=rate, output="sos"),
+            scipy.signal.butter(4, hi, btype="highpass", fs=rate, output="sos"))
+
+
+# ----------------------------------------------------------------------------
+# multiband (AME:196-210)
+# ----------------------------------------------------------------------------
+BAND_TIMES = ((10.0, 200.0), (5.0, 150.0), (1.0, 50.0))  # (attack, release) ms, AME:207-209
+
+
+def band_split(q: np.ndarray, rate):
+    lp, hp = crossover_sos(rate)
+    x = pcm_to_float(q)
+    lo = scipy.signal.sosfilt(lp, x, axis=0)
+    hi = scipy.signal.sosfilt(hp, x, axis=0)
+    mid = x - lo - hi
+    return quantize(lo), quantize(mid), quantize(hi)
+
+
+def overlay_add(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    return np.clip(a.astype(np.int32) + b.astype(np.int32), -32768, 32767).astype(np.int16)
+
+
+def multiband(q: np.ndarray, rate, thresholds, ratios):
+    bands = band_split(q, rate)
+    outs = [compress_band(b, rate, t, r, at, rel)
+            for b, t, r, (at, rel) in zip(bands, thresholds, ratios, BAND_TIMES)]
+    return overlay_add(overlay_add(outs[0], outs[1]), outs[2])
+
+
+def multiband_params(settings):
+    return ((settings.get("low_thresh", -25.0), settings.get("mid_thresh", -20.0), settings.get("high_thresh", -15.0)),
+            (settings.get("low_ratio", 6.0), settings.get("mid_ratio", 3.0), settings.get("high_ratio", 4.0)))
+
+
+# ----------------------------------------------------------------------------
+# loudness (pyloudnorm restated) and normalisation (AME:212-222)
+# ----------------------------------------------------------------------------
+def integrated_loudness(mono: np.ndarray, rate) -> float:
+    return tp.Meter(rate).integrated_loudness(mono)
+
+
+def normalize_to_lufs(y: np.ndarray, rate, target):
+    mono = y.mean(axis=1) if y.ndim == 2 else y
+    L = integrated_loudness(mono, rate)
+    gain = 10.0 ** ((target - L) / 20.0)
+    with np.errstate(invalid="ignore", over="ignore"):
+        return y * gain, L
+
+
+# ----------------------------------------------------------------------------
+# chunking (AME:48-54 through pydub ms slicing)
+# ----------------------------------------------------------------------------
+def chunk_ranges(frames: int, rate: int, chunk_ms: int = 30000):
+    """[(start_frame, stop_frame)] as pydub's `audio[s:s+30000]` computes them;
+    stop may exceed `frames` (pydub pads <=2 ms of silence)."""
+    n_ms = round(1000 * (frames / rate))
+    out = []
+    for s in range(0, n_ms, chunk_ms):
+        e = min(s + chunk_ms, n_ms)
+        out.append((int(s * (rate / 1000.0)), int(e * (rate / 1000.0))))
+    return out
+
+
+def master(pcm: np.ndarray, rate: int, settings: dict, return_loudness: bool = False):
+    """Full AME chain on int16 PCM [N] or [N, ch] -> int16 PCM (same layout)."""
+    stereo = pcm.ndim == 2
+    ch = pcm.shape[1] if stereo else 1
+    if ch == 1 and stereo:
+        pcm = pcm[:, 0]
+        stereo = False
+    N = pcm.shape[0]
+    thr, rat = multiband_params(settings)
+    chunks = []
+    for s, e in chunk_ranges(N, rate):
+        c = pcm[s:min(e, N)]
+        if e > N:
+            pad = np.zeros((e - N,) + pcm.shape[1:], np.int16)
+            c = np.concatenate([c, pad])
+        x = pcm_to_float(c)
+        x = saturation(x, settings.get("saturation", 0))
+        x = equalize(x, rate, settings)
+        if settings.get("width", 1.0) != 1.0:
+            x = stereo_width(x, settings.get("width"))
+        q = quantize(x)
+        if settings.get("multiband"):
+            q = multiband(q, rate, thr, rat)
+        chunks.append(q)
+    out = np.concatenate(chunks) if chunks else np.zeros((0,) + pcm.shape[1:], np.int16)
+    y = pcm_to_float(out)
+    L = None
+    if settings.get("lufs") is not None:
+        y, L = normalize_to_lufs(y, rate, settings.get("lufs"))
+    with np.errstate(invalid="ignore"):
+        y = soft_limiter(y)
+        res = quantize(y)
+    return (res, L) if return_loudness else res

@@ -1,0 +1,662 @@
+// kernels.hip — CDNA4 (gfx950) kernels of the mastering chain.
+//
+// Layout: a track's processed timeline (AME:48-54 chunking) is cut into tiles of
+// T frames; every 30 s chunk is a whole number of tiles (T | chunk frames), so a
+// chunk never shares a tile.  One lane owns one tile and walks it sequentially
+// (the IIR / envelope recurrences are sequential in time); lanes of a wave own
+// consecutive tiles.  Intermediates are stored TILE-MAJOR: element (tile g,
+// frame n) lives at n*G + g, so at every step a wave's 64 lanes touch 64
+// consecutive elements -> fully coalesced HBM/L2 traffic for every pass after
+// ingest.  Linear recurrences (EQ, crossover, K-weighting) use the two-pass block
+// method: pass 1 = zero-state end state per tile, a scan of affine state maps
+// across tiles (scan.hip), pass 2 = exact re-run from the carried state.
+#include "common.h"
+
+namespace mm {
+
+// ---------------------------------------------------------------- pointwise
+
+// float_array_to_audio_segment (AME:123-126): clip to [-1,1] (NaN propagates),
+// * 32768, astype(int16) == trunc to int32 then wrap to 16 bits; NaN -> 0.
+__device__ __forceinline__ int16_t quantize(double v) {
+    if (v != v) return 0;
+    v = v > 1.0 ? 1.0 : v;
+    v = v < -1.0 ? -1.0 : v;
+    int32_t i = (int32_t)(v * 32768.0);
+    return (int16_t)i;
+}
+
+// apply_saturation (AME:128-134), f32 throughout; no FMA contraction so the
+// rounding sequence matches numpy: keep*x + mix*tanh(x*drive).
+__device__ __forceinline__ float saturate(float x, const SatArgs &s) {
+    float t = tanhf(__fmul_rn(x, s.drive));
+    return __fadd_rn(__fmul_rn(s.keep, x), __fmul_rn(s.mix, t));
+}
+
+// audioop.mul of one int16 sample (pydub compressor output, AME:207-209).
+__device__ __forceinline__ int16_t audioop_mul(int16_t x, double g) {
+    double v = (double)x * g;
+    if (v > 32767.0) v = 32767.0;
+    else if (v < -32767.0) v = -32768.0;
+    return (int16_t)(int32_t)floor(v);
+}
+
+__device__ __forceinline__ int16_t sat16(int32_t v) {
+    return (int16_t)(v > 32767 ? 32767 : (v < -32768 ? -32768 : v));
+}
+
+// ---------------------------------------------------------------- biquads
+// DF2T section (scipy sosfilt / lfilter form): y = b0 x + z0;
+// z0 = b1 x - a1 y + z1; z1 = b2 x - a2 y.  State s = (z0, z1).
+__device__ __forceinline__ double df2t(double x, double &z0, double &z1, const double *c) {
+    double y = fma(c[0], x, z0);
+    z0 = fma(c[1], x, fma(-c[3], y, z1));
+    z1 = fma(c[2], x, -c[4] * y);
+    return y;
+}
+
+template <int NS>
+__device__ __forceinline__ double cascade(double x, double (&z)[NS][2], const double (*sos)[5]) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) x = df2t(x, z[s][0], z[s][1], sos[s]);
+    return x;
+}
+
+// ------------------------------------------------------- stage A: pre-chain
+// Input: natural interleaved f32 (PCM16/32768), frames >= N_in read as 0
+// (pydub pads a short final slice with silence).  Saturation f32, EQ cascade
+// f64 (each active AME stage is one sosfilt section; zero-gain stages are
+// dropped on the host), width f64, quantise -> q1 (tile-major short2).
+
+__device__ __forceinline__ void load_in(const float *in, int64_t f, int64_t N_in, int ch, float &l, float &r) {
+    if (f < N_in) {
+        if (ch == 2) {
+            float2 v = *reinterpret_cast<const float2 *>(in + 2 * f);
+            l = v.x;
+            r = v.y;
+        } else {
+            l = in[f];
+            r = 0.f;
+        }
+    } else {
+        l = 0.f;
+        r = 0.f;
+    }
+}
+
+template <int NS, bool PASS2>
+__global__ void __launch_bounds__(256) eq_kernel(StageArgs a) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= a.G) return;
+    const int64_t f0 = g * a.T;
+    const int len = (int)min((int64_t)a.T, a.N_proc - f0);
+    const int ch = a.ch;
+    constexpr int D = 8;  // state stride per channel (MM_MAX_DIM), unused entries 0
+    double zl[NS][2], zr[NS][2];
+    if (PASS2) {
+        const double *s = a.s_in + (g * ch) * D;
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            zl[k][0] = s[2 * k];
+            zl[k][1] = s[2 * k + 1];
+            if (ch == 2) {
+                zr[k][0] = s[D + 2 * k];
+                zr[k][1] = s[D + 2 * k + 1];
+            } else {
+                zr[k][0] = zr[k][1] = 0.0;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < NS; ++k) zl[k][0] = zl[k][1] = zr[k][0] = zr[k][1] = 0.0;
+    }
+    const double(*sos)[5] = a.sos;
+    for (int n = 0; n < len; ++n) {
+        float l, r;
+        load_in(a.in, f0 + n, a.N_in, ch, l, r);
+        if (a.sat.on) {
+            l = saturate(l, a.sat);
+            r = saturate(r, a.sat);
+        }
+        double yl = cascade<NS>((double)l, zl, sos);
+        double yr = ch == 2 ? cascade<NS>((double)r, zr, sos) : 0.0;
+        if (PASS2) {
+            if (a.width_on) {  // apply_stereo_width (AME:136-144) in f64
+                double mid = (yl + yr) / 2;
+                double side = (yl - yr) / 2 * a.width;
+                yl = mid + side;
+                yr = mid - side;
+            }
+            short2 q;
+            q.x = quantize(yl);
+            q.y = quantize(yr);
+            a.q_out[(int64_t)n * a.G + g] = q;
+        }
+    }
+    if (!PASS2) {
+        double *z = a.z_out + (g * ch) * D;
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            z[2 * k] = zl[k][0];
+            z[2 * k + 1] = zl[k][1];
+            if (ch == 2) {
+                z[D + 2 * k] = zr[k][0];
+                z[D + 2 * k + 1] = zr[k][1];
+            }
+        }
+        for (int k = 2 * NS; k < D; ++k) {
+            z[k] = 0.0;
+            if (ch == 2) z[D + k] = 0.0;
+        }
+    }
+}
+
+// No active EQ stage: the chain stays f32 (AME:152-162 returns the f32 input;
+// width then runs in f32).
+__global__ void __launch_bounds__(256) pre_pointwise_kernel(StageArgs a) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= a.G) return;
+    const int64_t f0 = g * a.T;
+    const int len = (int)min((int64_t)a.T, a.N_proc - f0);
+    for (int n = 0; n < len; ++n) {
+        float l, r;
+        load_in(a.in, f0 + n, a.N_in, a.ch, l, r);
+        if (a.sat.on) {
+            l = saturate(l, a.sat);
+            r = saturate(r, a.sat);
+        }
+        if (a.width_on) {
+            float w = (float)a.width;
+            float mid = __fdiv_rn(__fadd_rn(l, r), 2.0f);
+            float side = __fmul_rn(__fdiv_rn(__fsub_rn(l, r), 2.0f), w);
+            l = __fadd_rn(mid, side);
+            r = __fsub_rn(mid, side);
+        }
+        short2 q;
+        q.x = quantize((double)l);
+        q.y = a.ch == 2 ? quantize((double)r) : (int16_t)0;
+        a.q_out[(int64_t)n * a.G + g] = q;
+    }
+}
+
+// ------------------------------------------------------ stage B: crossover
+// apply_multiband_compressor (AME:196-206): x = int16/32768 (f32), LP = butter(4)
+// 250 Hz (2 SOS), HP = butter(4) 4 kHz (2 SOS), f64; mid = (x - lo) - hi;
+// each band quantised.  Two branches of 2 sections share the input.
+template <bool PASS2>
+__global__ void __launch_bounds__(256) xover_kernel(StageArgs a) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= a.G) return;
+    const int64_t f0 = g * a.T;
+    const int len = (int)min((int64_t)a.T, a.N_proc - f0);
+    const int ch = a.ch;
+    constexpr int D = 8;
+    double lo[2][2][2], hi[2][2][2];  // [channel][section][z]
+    for (int c = 0; c < 2; ++c)
+        for (int k = 0; k < 2; ++k) {
+            if (PASS2 && c < ch) {
+                const double *s = a.s_in + (g * ch + c) * D;
+                lo[c][k][0] = s[2 * k];
+                lo[c][k][1] = s[2 * k + 1];
+                hi[c][k][0] = s[4 + 2 * k];
+                hi[c][k][1] = s[4 + 2 * k + 1];
+            } else {
+                lo[c][k][0] = lo[c][k][1] = hi[c][k][0] = hi[c][k][1] = 0.0;
+            }
+        }
+    const double(*sos)[5] = a.sos;
+    for (int n = 0; n < len; ++n) {
+        const int64_t idx = (int64_t)n * a.G + g;
+        short2 q = a.q_in[idx];
+        double x[2] = {(double)((float)q.x / 32768.0f), (double)((float)q.y / 32768.0f)};
+        short2 qb[3];
+        int16_t *qbl = reinterpret_cast<int16_t *>(qb);
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            if (c >= ch) {
+                qbl[0 + c] = qbl[2 + c] = qbl[4 + c] = 0;
+                continue;
+            }
+            double yl = df2t(x[c], lo[c][0][0], lo[c][0][1], sos[0]);
+            yl = df2t(yl, lo[c][1][0], lo[c][1][1], sos[1]);
+            double yh = df2t(x[c], hi[c][0][0], hi[c][0][1], sos[2]);
+            yh = df2t(yh, hi[c][1][0], hi[c][1][1], sos[3]);
+            if (PASS2) {
+                double ym = (x[c] - yl) - yh;
+                qbl[0 + c] = quantize(yl);
+                qbl[2 + c] = quantize(ym);
+                qbl[4 + c] = quantize(yh);
+            }
+        }
+        if (PASS2) {
+            a.band_out[0][idx] = qb[0];
+            a.band_out[1][idx] = qb[1];
+            a.band_out[2][idx] = qb[2];
+        }
+    }
+    if (!PASS2) {
+        for (int c = 0; c < ch; ++c) {
+            double *z = a.z_out + (g * ch + c) * D;
+            for (int k = 0; k < 2; ++k) {
+                z[2 * k] = lo[c][k][0];
+                z[2 * k + 1] = lo[c][k][1];
+                z[4 + 2 * k] = hi[c][k][0];
+                z[4 + 2 * k + 1] = hi[c][k][1];
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------ stage C: compressor
+// pydub compress_dynamic_range per band (AME:207-209), restated in SURVEY.md
+// Appendix A.  rms over frames [max(chunk0, i-look), i) (excludes i), both
+// channels: audioop.rms = (unsigned)sqrt(S/n) which, for integer S and
+// n <= 2^12, equals isqrt(S div n) exactly (proved in DESIGN.md, checked in
+// tests).  Max attenuation M(rms) comes from a host table built with pydub's
+// own float expressions; inc/dec are M/attack_frames, M/release_frames
+// (correctly rounded).  'above' (rms > thresh) == (M != 0).
+
+__device__ __forceinline__ uint32_t rms_exact(int64_t S, int64_t n) {
+    if (n <= 0) return 0;
+    double q = (double)S / (double)n;
+    int64_t r = (int64_t)sqrt(q);
+    // integer fix-up: largest r with n*r*r <= S
+    while (r > 0 && n * r * r > S) --r;
+    while (n * (r + 1) * (r + 1) <= S) ++r;
+    return (uint32_t)r;
+}
+
+__device__ __forceinline__ int32_t frame_energy(short2 v) {
+    return (int32_t)v.x * v.x + (int32_t)v.y * v.y;
+}
+
+// M[b][n*G+g] for every frame.  grid: (ceil(G/256), 3 bands)
+__global__ void __launch_bounds__(256) comp_rms_kernel(CompArgs a) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int b = blockIdx.y;
+    if (g >= a.G) return;
+    const short2 *x = a.band[b];
+    const double *lut = a.max_att[b];
+    const int look = a.look[b];
+    const int64_t f0 = g * a.T;
+    const int64_t chunk0 = (g / a.K) * a.K * a.T;
+    const int len = (int)min((int64_t)a.T, a.N_proc - f0);
+    // initial window [max(chunk0, f0-look), f0)
+    int64_t lo = max(chunk0, f0 - look);
+    int64_t S = 0;
+    for (int64_t f = lo; f < f0; ++f) {
+        int64_t gg = f / a.T, nn = f - gg * a.T;
+        S += frame_energy(x[nn * a.G + gg]);
+    }
+    const int ch = a.ch;
+    double *M = a.M[b];
+    for (int n = 0; n < len; ++n) {
+        const int64_t f = f0 + n;
+        const int64_t cnt = (f - lo) * ch;
+        uint32_t r = rms_exact(S, cnt);
+        M[(int64_t)n * a.G + g] = lut[r];
+        // slide: add frame f, drop frame f-look if it was in the window
+        S += frame_energy(x[(int64_t)n * a.G + g]);
+        int64_t drop = f - look;
+        if (drop >= lo) {
+            int64_t gg = drop / a.T, nn = drop - gg * a.T;
+            S -= frame_energy(x[nn * a.G + gg]);
+            lo = drop + 1;
+        }
+    }
+}
+
+// correctly rounded m / d given rd = RN(1/d) (Markstein)
+__device__ __forceinline__ double div_cr(double m, double d, double rd) {
+    double q = m * rd;
+    double rem = fma(-q, d, m);
+    return fma(rem, rd, q);
+}
+
+struct BandStep {
+    double A, R, rA, rR;
+};
+
+__device__ __forceinline__ double comp_step(double att, double M, const BandStep &bs) {
+    if (M != 0.0 && att <= M) {
+        double inc = div_cr(M, bs.A, bs.rA);
+        att = att + inc;
+        att = (M < att) ? M : att;
+    } else {
+        double dec = div_cr(M, bs.R, bs.rR);
+        att = att - dec;
+        att = (0.0 > att) ? 0.0 : att;
+    }
+    return att;
+}
+
+__device__ __forceinline__ BandStep band_step(const CompArgs &a, int b) {
+    BandStep s;
+    s.A = a.attack_frames[b];
+    s.R = a.release_frames[b];
+    s.rA = a.rcp_attack[b];
+    s.rR = a.rcp_release[b];
+    return s;
+}
+
+// Speculative pass: each (tile, band) starts from a warm-up run of W frames
+// (from 0) before its first frame; tile 0 of a chunk starts exactly at 0.
+// Also flags identity tiles (every frame has M == 0: att is held exactly).
+// grid: (ceil(G/256), 3)
+__global__ void __launch_bounds__(256) comp_pass0_kernel(CompArgs a) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int b = blockIdx.y;
+    if (g >= a.G) return;
+    const BandStep bs = band_step(a, b);
+    const double *M = a.M[b];
+    const int64_t f0 = g * a.T;
+    const int64_t chunk0 = (g / a.K) * a.K * a.T;
+    const int len = (int)min((int64_t)a.T, a.N_proc - f0);
+    double att = 0.0;
+    for (int64_t f = max(chunk0, f0 - a.warmup); f < f0; ++f) {
+        int64_t gg = f / a.T, nn = f - gg * a.T;
+        att = comp_step(att, M[nn * a.G + gg], bs);
+    }
+    a.start[b][g] = att;
+    int ident = 1;
+    for (int n = 0; n < len; ++n) {
+        double m = M[(int64_t)n * a.G + g];
+        ident &= (m == 0.0);
+        att = comp_step(att, m, bs);
+    }
+    a.end_out[b][g] = att;
+    a.ident[b][g] = ident;
+}
+
+// prev_active[g] = largest p < g in g's chunk with !ident[p], else -1.
+// One 1024-thread block per (chunk, band): serial runs + Kogge-Stone max-scan.
+__global__ void __launch_bounds__(1024) comp_prev_active_kernel(CompArgs a) {
+    __shared__ int64_t buf[1024];
+    const int b = blockIdx.y;
+    const int64_t t0 = (int64_t)blockIdx.x * a.K;
+    const int64_t n = min((int64_t)a.K, a.G - t0);
+    const int64_t c = (n + 1023) / 1024;
+    const int tid = threadIdx.x;
+    const int64_t b0 = tid * c, b1 = min(b0 + c, n);
+    int64_t last = -1;
+    for (int64_t m = b0; m < b1; ++m)
+        if (!a.ident[b][t0 + m]) last = t0 + m;
+    buf[tid] = last;
+    __syncthreads();
+    int64_t v = last;
+    for (int d = 1; d < 1024; d <<= 1) {
+        int64_t o = tid >= d ? buf[tid - d] : -1;
+        __syncthreads();
+        v = max(v, o);
+        buf[tid] = v;
+        __syncthreads();
+    }
+    int64_t run = tid > 0 ? buf[tid - 1] : -1;
+    for (int64_t m = b0; m < b1; ++m) {
+        a.prev_active[b][t0 + m] = (int32_t)run;
+        if (!a.ident[b][t0 + m]) run = t0 + m;
+    }
+}
+
+// One Jacobi sweep: an active tile whose start differs from the end of its
+// nearest active predecessor (identity tiles in between hold att exactly) is
+// re-run from that end.  Exact at convergence (every start == true state).
+__global__ void __launch_bounds__(256) comp_fix_kernel(CompArgs a) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int b = blockIdx.y;
+    if (g >= a.G) return;
+    const double *end_in = a.end_in[b];
+    double e = end_in[g];
+    if (!a.ident[b][g]) {
+        const int32_t p = a.prev_active[b][g];
+        double want = p >= 0 ? end_in[p] : 0.0;
+        double have = a.start[b][g];
+        if (__double_as_longlong(want) != __double_as_longlong(have)) {
+            const BandStep bs = band_step(a, b);
+            const double *M = a.M[b];
+            const int64_t f0 = g * a.T;
+            const int len = (int)min((int64_t)a.T, a.N_proc - f0);
+            double att = want;
+            for (int n = 0; n < len; ++n) att = comp_step(att, M[(int64_t)n * a.G + g], bs);
+            a.start[b][g] = want;
+            e = att;
+            atomicAdd(a.changed, 1u);
+        }
+    }
+    a.end_out[b][g] = e;
+}
+
+// Final pass: exact trajectory from the converged starts; gains applied to the
+// three band samples (audioop.mul floor), overlay sat16(sat16(lo+mid)+hi)
+// (AME:210) -> q2.
+__global__ void __launch_bounds__(256) comp_apply_kernel(CompArgs a) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= a.G) return;
+    BandStep bs[3];
+    double att[3];
+    for (int b = 0; b < 3; ++b) {
+        bs[b] = band_step(a, b);
+        if (a.ident[b][g]) {  // held tile: att == end of the nearest active predecessor
+            const int32_t p = a.prev_active[b][g];
+            att[b] = p >= 0 ? a.end_in[b][p] : 0.0;
+        } else {
+            att[b] = a.start[b][g];
+        }
+    }
+    const int64_t f0 = g * a.T;
+    const int len = (int)min((int64_t)a.T, a.N_proc - f0);
+    for (int n = 0; n < len; ++n) {
+        const int64_t idx = (int64_t)n * a.G + g;
+        int32_t accl = 0, accr = 0;
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            att[b] = comp_step(att[b], a.M[b][idx], bs[b]);
+            short2 v = a.band[b][idx];
+            if (att[b] != 0.0) {
+                double gain = exp10(-att[b] / 20.0);
+                v.x = audioop_mul(v.x, gain);
+                v.y = audioop_mul(v.y, gain);
+            }
+            if (b == 0) {
+                accl = v.x;
+                accr = v.y;
+            } else {
+                accl = sat16(accl + v.x);
+                accr = sat16(accr + v.y);
+            }
+        }
+        short2 o;
+        o.x = (int16_t)accl;
+        o.y = a.ch == 2 ? (int16_t)accr : (int16_t)0;
+        a.q_out[idx] = o;
+    }
+}
+
+// ------------------------------------------------- stage D: K-weighting
+// pyloudnorm Meter (AME:213-218): mono = f32 mean(L,R) (= (L+R)/65536 exactly),
+// high_shelf lfilter in f64 stored back to f32, high_pass lfilter in f64
+// stored to f32, then squared sums per 0.4 s/0.1 s block.  The whole track is
+// one line (state carries across chunks).  Pass 2 accumulates per-tile partial
+// energies of the (at most two) loudness segments the tile touches.
+template <bool PASS2>
+__global__ void __launch_bounds__(256) kweight_kernel(KwArgs a) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= a.G) return;
+    const int64_t f0 = g * a.T;
+    const int len = (int)min((int64_t)a.T, a.N_proc - f0);
+    double z[2][2];
+    if (PASS2) {
+        const double *s = a.s_in + g * 4;
+        z[0][0] = s[0];
+        z[0][1] = s[1];
+        z[1][0] = s[2];
+        z[1][1] = s[3];
+    } else {
+        z[0][0] = z[0][1] = z[1][0] = z[1][1] = 0.0;
+    }
+    // segment bookkeeping
+    int64_t seg = 0, seg_end = 0;
+    if (PASS2) {
+        // largest s with bounds[s] <= f0
+        int64_t lo = 0, hi = a.n_segs;  // bounds has n_segs+1 entries
+        while (hi - lo > 1) {
+            int64_t mid = (lo + hi) >> 1;
+            if (a.seg_bounds[mid] <= f0) lo = mid;
+            else hi = mid;
+        }
+        seg = lo;
+        seg_end = a.seg_bounds[seg + 1];
+    }
+    double e0 = 0.0, e1 = 0.0;
+    bool second = false;
+    for (int n = 0; n < len; ++n) {
+        short2 q = a.mix[(int64_t)n * a.G + g];
+        float m = a.ch == 2 ? ((float)q.x + (float)q.y) * (1.0f / 65536.0f) : (float)q.x * (1.0f / 32768.0f);
+        double y1 = df2t((double)m, z[0][0], z[0][1], a.sos[0]);
+        float y1f = (float)y1;
+        double y2 = df2t((double)y1f, z[1][0], z[1][1], a.sos[1]);
+        if (PASS2) {
+            float y2f = (float)y2;
+            double e = (double)y2f * (double)y2f;
+            if (f0 + n >= seg_end) {
+                second = true;
+                seg_end = 0x7fffffffffffffffLL;
+            }
+            if (second) e1 += e;
+            else e0 += e;
+        }
+    }
+    if (PASS2) {
+        a.part[2 * g] = e0;
+        a.part[2 * g + 1] = e1;
+        a.part_seg[g] = seg;
+    } else {
+        double *zo = a.z_out + g * 4;
+        zo[0] = z[0][0];
+        zo[1] = z[0][1];
+        zo[2] = z[1][0];
+        zo[3] = z[1][1];
+    }
+}
+
+// Sum the per-tile partials into loudness segments (deterministic order).
+__global__ void seg_reduce_kernel(KwArgs a, double *seg_energy) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= a.n_segs) return;
+    int64_t b0 = a.seg_bounds[s], b1 = a.seg_bounds[s + 1];
+    if (b1 > a.N_proc) b1 = a.N_proc;
+    double acc = 0.0;
+    if (b0 < b1) {
+        int64_t g0 = b0 / a.T, g1 = (b1 - 1) / a.T;
+        for (int64_t g = g0; g <= g1; ++g) {
+            if (a.part_seg[g] == s) acc += a.part[2 * g];
+            else if (a.part_seg[g] == s - 1) acc += a.part[2 * g + 1];
+        }
+    }
+    seg_energy[s] = acc;
+}
+
+// ------------------------------------------------ stage E: gain + limiter
+// AME:84-89: y = int16/32768 (f32); with a loudness target the gain is an
+// np.float64 so y*gain, the soft limiter and the clip run in f64; without
+// one they run in f32.  Output natural interleaved layout.  A block handles
+// 64 tiles: the tile-major mix is read coalesced into LDS, then written out
+// frame-major coalesced.
+constexpr int FIN_TILES = 64;
+
+__device__ __forceinline__ double limiter64(double y) {
+    double ay = fabs(y);
+    if (ay > 0.98) {
+        double d = ay - 0.98;
+        double t = d / 0.02;
+        double den = sqrt(1.0 + t * t);
+        double v = 0.98 + d / den;
+        double sg = y > 0 ? 1.0 : (y < 0 ? -1.0 : y);
+        y = v * sg;
+    }
+    return y;
+}
+
+__device__ __forceinline__ float limiter32(float y) {
+    float ay = fabsf(y);
+    if (ay > 0.98f) {
+        float d = __fsub_rn(ay, 0.98f);
+        float t = __fdiv_rn(d, 0.02f);
+        float den = __fsqrt_rn(__fadd_rn(1.0f, __fmul_rn(t, t)));
+        float v = __fadd_rn(0.98f, __fdiv_rn(d, den));
+        float sg = y > 0 ? 1.0f : (y < 0 ? -1.0f : y);
+        y = __fmul_rn(v, sg);
+    }
+    return y;
+}
+
+__global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
+    extern __shared__ short2 lds[];  // [FIN_TILES][T+1]
+    const int T = a.T;
+    const int stride = T + 1;
+    const int64_t g0 = (int64_t)blockIdx.x * FIN_TILES;
+    const int ntile = (int)min((int64_t)FIN_TILES, a.G - g0);
+    // load: row n, lanes over tiles
+    for (int i = threadIdx.x; i < T * FIN_TILES; i += blockDim.x) {
+        int n = i / FIN_TILES, t = i - n * FIN_TILES;
+        if (t < ntile) lds[t * stride + n] = a.mix[(int64_t)n * a.G + g0 + t];
+    }
+    __syncthreads();
+    const int64_t f_base = g0 * T;
+    const int64_t nf = min((int64_t)ntile * T, a.N_proc - f_base);
+    for (int64_t i = threadIdx.x; i < nf; i += blockDim.x) {
+        int t = (int)(i / T), n = (int)(i - (int64_t)t * T);
+        short2 q = lds[t * stride + n];
+        int16_t o[2];
+        int16_t qq[2] = {q.x, q.y};
+        for (int c = 0; c < a.ch; ++c) {
+            float y = (float)qq[c] / 32768.0f;
+            if (a.use_gain) {
+                double v = (double)y * a.gain;
+                o[c] = quantize(limiter64(v));
+            } else {
+                o[c] = quantize((double)limiter32(y));
+            }
+        }
+        const int64_t f = f_base + i;
+        if (a.out_kind == 0) {
+            int16_t *out = reinterpret_cast<int16_t *>(a.out);
+            if (a.ch == 2) *reinterpret_cast<short2 *>(out + 2 * f) = make_short2(o[0], o[1]);
+            else out[f] = o[0];
+        } else {
+            float *out = reinterpret_cast<float *>(a.out);
+            if (a.ch == 2) *reinterpret_cast<float2 *>(out + 2 * f) = make_float2(o[0] / 32768.0f, o[1] / 32768.0f);
+            else out[f] = o[0] / 32768.0f;
+        }
+    }
+}
+
+// copy the tile-major mix to natural interleaved int16 (parity probe)
+__global__ void mix_to_natural_kernel(const short2 *mix, int16_t *out, int64_t G, int T, int64_t N, int ch) {
+    const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= N) return;
+    int64_t g = f / T, n = f - g * T;
+    short2 q = mix[n * G + g];
+    if (ch == 2) {
+        out[2 * f] = q.x;
+        out[2 * f + 1] = q.y;
+    } else {
+        out[f] = q.x;
+    }
+}
+
+// explicit instantiations used by the host
+template __global__ void eq_kernel<1, false>(StageArgs);
+template __global__ void eq_kernel<2, false>(StageArgs);
+template __global__ void eq_kernel<3, false>(StageArgs);
+template __global__ void eq_kernel<4, false>(StageArgs);
+template __global__ void eq_kernel<1, true>(StageArgs);
+template __global__ void eq_kernel<2, true>(StageArgs);
+template __global__ void eq_kernel<3, true>(StageArgs);
+template __global__ void eq_kernel<4, true>(StageArgs);
+template __global__ void xover_kernel<false>(StageArgs);
+template __global__ void xover_kernel<true>(StageArgs);
+template __global__ void kweight_kernel<false>(KwArgs);
+template __global__ void kweight_kernel<true>(KwArgs);
+
+}  // namespace mm

@@ -1,0 +1,10 @@
+"""mastering_amd — MI355X-native drop-in for the reference's mastering hot path.
+
+Public surface (mirrors worker/audio_mastering_engine.py):
+  EQ_PRESETS                   AME:15-20
+  process(in, out, params)     AME:24-113 with local WAV IO instead of GCS
+  master_pcm(pcm, rate, params)  the chain on an in-memory PCM array
+"""
+from .engine import EQ_PRESETS, Job, master_device, master_pcm, process  # noqa: F401
+
+__all__ = ["EQ_PRESETS", "Job", "master_pcm", "master_device", "process"]

@@ -1,0 +1,253 @@
+"""Host-side design of one mastering job (f64, the reference's own expressions).
+
+Everything here is small, per-job and exact: filter coefficients, the compressor's
+max-attenuation tables, chunk/tile geometry, IIR state-transition powers for the
+tile scan and pyloudnorm's block geometry.  The per-sample work runs in the HIP
+library; nothing here touches audio samples.
+
+Reference anchors (worker/audio_mastering_engine.py = "AME"):
+  chunking            AME:48-54 via pydub ms slicing (`len`, `__getitem__`)
+  saturation consts   AME:131-134
+  shelf / peak EQ     AME:170-194 (note: w0 = 4*pi*f/fs and gain = 10^(dB/20),
+                      exactly as written; we reproduce, not "fix", the formula)
+  crossover           AME:197-198 scipy.signal.butter(4, ..., output='sos')
+  compressor consts   pydub compress_dynamic_range via AME:207-209
+  K-weighting         pyloudnorm Meter(rate) filters via AME:213
+  loudness blocks     pyloudnorm integrated_loudness via AME:218
+"""
+from __future__ import annotations
+
+import functools
+import math
+
+import numpy as np
+import scipy.signal
+
+MAX_DIM = 8
+SCAN_POWERS = 12
+SCAN_THREADS = 1024
+CHUNK_MS = 30 * 1000  # AME:48
+DEFAULT_TILE = 250     # divides 30 s chunks at every rate that is a multiple of 25 Hz
+
+EQ_KEYS = ("bass_boost", "mid_cut", "presence_boost", "treble_boost")
+BAND_TIMES = ((10.0, 200.0), (5.0, 150.0), (1.0, 50.0))  # (attack, release) ms, AME:207-209
+BAND_DEFAULTS = (("low_thresh", -25.0, "low_ratio", 6.0),
+                 ("mid_thresh", -20.0, "mid_ratio", 3.0),
+                 ("high_thresh", -15.0, "high_ratio", 4.0))  # AME:67-72
+
+
+# ----------------------------------------------------------------- chunking
+def pydub_len_ms(frames: int, rate: int) -> int:
+    """pydub AudioSegment.__len__: round(1000 * frames / rate)."""
+    return round(1000 * (float(frames) / rate))
+
+
+def pydub_frame(ms, rate: int) -> int:
+    """pydub _parse_position: int(ms * (rate / 1000.0))."""
+    return int(ms * (rate / 1000.0))
+
+
+def chunk_bounds(frames: int, rate: int):
+    """Frame ranges of AME's `for start_ms in range(0, len(audio), 30000)` slices.
+    The stop of the last slice may exceed `frames` (pydub pads <= 2 ms of silence)
+    or fall short of it (frames past the last whole ms are dropped)."""
+    n_ms = pydub_len_ms(frames, rate)
+    out = []
+    for s in range(0, n_ms, CHUNK_MS):
+        e = min(s + CHUNK_MS, n_ms)
+        a, b = pydub_frame(s, rate), pydub_frame(e, rate)
+        if b - min(b, frames) > (2 * (rate / 1000.0)):
+            raise ValueError("TooManyMissingFrames")
+        out.append((a, b))
+    return out
+
+
+def choose_tile(chunk_frames: int, preferred: int = DEFAULT_TILE) -> int:
+    if chunk_frames % preferred == 0:
+        return preferred
+    best = 0
+    for t in range(512, 63, -1):
+        if chunk_frames % t == 0:
+            best = t
+            break
+    if not best:
+        raise NotImplementedError(
+            f"no tile length in [64, 512] divides the {chunk_frames}-frame chunk; rate unsupported")
+    return best
+
+
+# --------------------------------------------------------------- EQ (AME:146-194)
+def shelf_section(rate, cutoff_hz, gain_db, kind, q=0.707):
+    """apply_shelf_filter coefficients (AME:170-182) -> (b0, b1, b2, a1, a2)."""
+    nyq = 0.5 * rate
+    wn = cutoff_hz / nyq
+    g = 10.0 ** (gain_db / 20.0)
+    cw = np.cos(wn * 2 * np.pi)
+    alpha = np.sin(wn * 2 * np.pi) / (2.0 * q)
+    sq = np.sqrt(g)
+    if kind == "low":
+        b0 = g * ((g + 1) - (g - 1) * cw + 2 * sq * alpha)
+        b1 = 2 * g * ((g - 1) - (g + 1) * cw)
+        b2 = g * ((g + 1) - (g - 1) * cw - 2 * sq * alpha)
+        a0 = (g + 1) + (g - 1) * cw + 2 * sq * alpha
+        a1 = -2 * ((g - 1) + (g + 1) * cw)
+        a2 = (g + 1) + (g - 1) * cw - 2 * sq * alpha
+    else:
+        b0 = g * ((g + 1) + (g - 1) * cw + 2 * sq * alpha)
+        b1 = -2 * g * ((g - 1) + (g + 1) * cw)
+        b2 = g * ((g + 1) + (g - 1) * cw - 2 * sq * alpha)
+        a0 = (g + 1) - (g - 1) * cw + 2 * sq * alpha
+        a1 = 2 * ((g - 1) - (g + 1) * cw)
+        a2 = (g + 1) - (g - 1) * cw - 2 * sq * alpha
+    return (b0 / a0, b1 / a0, b2 / a0, a1 / a0, a2 / a0)
+
+
+def peak_section(rate, center_hz, gain_db, q=1.0):
+    """apply_peak_filter coefficients (AME:185-193)."""
+    nyq = 0.5 * rate
+    wn = center_hz / nyq
+    g = 10.0 ** (gain_db / 20.0)
+    alpha = np.sin(wn * 2 * np.pi) / (2.0 * q)
+    b0, b1, b2 = 1 + alpha * g, -2 * np.cos(wn * 2 * np.pi), 1 - alpha * g
+    a0, a1, a2 = 1 + alpha / g, -2 * np.cos(wn * 2 * np.pi), 1 - alpha / g
+    return (b0 / a0, b1 / a0, b2 / a0, a1 / a0, a2 / a0)
+
+
+def eq_sections(rate, params):
+    """Active EQ sections in AME order (AME:154-161); 0 dB stages are skipped
+    (AME:171,186 `if gain_db == 0: return samples`)."""
+    bass, mid, pres, treb = (params.get(k, 0.0) for k in EQ_KEYS)
+    secs = []
+    if bass != 0:
+        secs.append(shelf_section(rate, 250, bass, "low"))
+    if -mid != 0:
+        secs.append(peak_section(rate, 1000, -mid))
+    if pres != 0:
+        secs.append(peak_section(rate, 4000, pres))
+    if treb != 0:
+        secs.append(shelf_section(rate, 8000, treb, "high"))
+    return secs
+
+
+def crossover_sections(rate, low_hz=250, high_hz=4000):
+    """AME:197-198: butter(4) LP and HP as 2 SOS sections each."""
+    lp = scipy.signal.butter(4, low_hz, btype="lowpass", fs=rate, output="sos")
+    hp = scipy.signal.butter(4, high_hz, btype="highpass", fs=rate, output="sos")
+    secs = []
+    for sos in (lp, hp):
+        for row in sos:
+            assert row[3] == 1.0
+            secs.append((row[0], row[1], row[2], row[4], row[5]))
+    return secs
+
+
+def kweight_sections(rate):
+    """pyloudnorm 0.1.1 K-weighting: high_shelf(G=4, Q=1/sqrt2, 1500 Hz) then
+    high_pass(G=0, Q=0.5, 38 Hz), RBJ forms normalised by a0."""
+    out = []
+    for G, Q, fc, kind in ((4.0, 1 / np.sqrt(2), 1500.0, "high_shelf"), (0.0, 0.5, 38.0, "high_pass")):
+        A = 10 ** (G / 40.0)
+        w0 = 2.0 * np.pi * (fc / rate)
+        alpha = np.sin(w0) / (2.0 * Q)
+        if kind == "high_shelf":
+            b = (A * ((A + 1) + (A - 1) * np.cos(w0) + 2 * np.sqrt(A) * alpha),
+                 -2 * A * ((A - 1) + (A + 1) * np.cos(w0)),
+                 A * ((A + 1) + (A - 1) * np.cos(w0) - 2 * np.sqrt(A) * alpha))
+            a = ((A + 1) - (A - 1) * np.cos(w0) + 2 * np.sqrt(A) * alpha,
+                 2 * ((A - 1) - (A + 1) * np.cos(w0)),
+                 (A + 1) - (A - 1) * np.cos(w0) - 2 * np.sqrt(A) * alpha)
+        else:
+            b = ((1 + np.cos(w0)) / 2, -(1 + np.cos(w0)), (1 + np.cos(w0)) / 2)
+            a = (1 + alpha, -2 * np.cos(w0), 1 - alpha)
+        bn = np.array(b) / a[0]
+        an = np.array(a) / a[0]
+        out.append((bn[0], bn[1], bn[2], an[1], an[2]))
+    return out
+
+
+# ------------------------------------------------------- tile-scan matrices
+def transition_matrix(sections, branches):
+    """One zero-input step of cascaded DF2T sections.  `branches` lists the number
+    of sections per branch; every branch is fed by the same input.  State per
+    section (z0, z1) in section order, padded to MAX_DIM."""
+    A = np.zeros((MAX_DIM, MAX_DIM))
+    nsec = len(sections)
+    for col in range(2 * nsec):
+        z = np.zeros(2 * nsec)
+        z[col] = 1.0
+        new = z.copy()
+        s = 0
+        for nb in branches:
+            x = 0.0
+            for _ in range(nb):
+                b0, b1, b2, a1, a2 = sections[s]
+                z0, z1 = z[2 * s], z[2 * s + 1]
+                y = b0 * x + z0
+                new[2 * s] = b1 * x - a1 * y + z1
+                new[2 * s + 1] = b2 * x - a2 * y
+                x = y
+                s += 1
+        A[: 2 * nsec, col] = new
+    return A
+
+
+def scan_tables(A, tile, line_tiles, last_len):
+    c = max(1, -(-line_tiles // SCAN_THREADS))
+    phi = np.linalg.matrix_power(A, tile)
+    base = np.linalg.matrix_power(phi, c)
+    pows = [base]
+    for _ in range(SCAN_POWERS - 1):
+        pows.append(pows[-1] @ pows[-1])
+    last = np.linalg.matrix_power(A, last_len)
+    return c, phi, np.stack(pows), last
+
+
+# ------------------------------------------------ compressor (pydub constants)
+def _ratio_to_db(ratio):
+    return 20 * math.log(float(ratio), 10)
+
+
+@functools.lru_cache(maxsize=64)
+def max_att_table(threshold, ratio):
+    """pydub compress_dynamic_range's max_attenuation as a function of the
+    integer audioop.rms value r in [0, 32768] (exact Python float expressions)."""
+    thresh_rms = (float(1 << 16) / 2) * (10 ** (float(threshold) / 20))
+    out = np.empty(32769, np.float64)
+    k = 1 - (1.0 / ratio)
+    for r in range(32769):
+        if r == 0:
+            dbo = 0.0
+        else:
+            dbo = max(_ratio_to_db(r / thresh_rms), 0)
+        out[r] = k * dbo
+    out.setflags(write=False)
+    return out, thresh_rms
+
+
+def band_constants(rate, threshold, ratio, attack, release):
+    table, thr = max_att_table(float(threshold), float(ratio))
+    af = attack * (rate / 1000.0)
+    rf = release * (rate / 1000.0)
+    return {"table": table, "thresh_rms": thr, "attack_frames": af, "release_frames": rf, "look": int(af)}
+
+
+# ---------------------------------------------------- loudness block geometry
+def loudness_blocks(frames: int, rate: int, block_size: float = 0.4):
+    """pyloudnorm integrated_loudness block bounds (clamped to the data)."""
+    T = frames / rate
+    step = 1.0 - 0.75
+    nblocks = int(np.round(((T - block_size) / (block_size * step)))) + 1
+    j = np.arange(0, nblocks)
+    lo = np.array([int(block_size * (jj * step) * rate) for jj in j], dtype=np.int64)
+    hi = np.array([int(block_size * (jj * step + 1) * rate) for jj in j], dtype=np.int64)
+    lo = np.minimum(lo, frames)
+    hi = np.minimum(hi, frames)
+    bounds = np.unique(np.concatenate([[0], lo, hi, [frames]]))
+    return nblocks, lo, hi, bounds.astype(np.int64), 1.0 / (block_size * rate)
+
+
+def saturation_consts(percent):
+    if percent == 0:
+        return 0, 1.0, 0.0, 1.0
+    mix = (percent / 100.0) ** 2
+    return 1, float(np.float32(1 - mix)), float(np.float32(mix)), float(np.float32(1 + mix * 4))
