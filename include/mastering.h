@@ -91,8 +91,10 @@ typedef struct mm_job {
     mm_iir xover;            /* butter(4) LP250 (branch 0) + HP4000 (branch 1)  */
     mm_iir kweight;          /* pyloudnorm high_shelf then high_pass            */
     mm_band band[3];         /* low / mid / high                                */
-    int32_t comp_warmup;     /* speculative warm-up frames per tile             */
+    int32_t comp_warmup;     /* >0: speculative warm-up over the previous super-tile */
     int32_t comp_max_iters;  /* cap on fix-up sweeps (exactness check)          */
+    int32_t comp_super;      /* tiles per super-tile of the envelope solve      */
+    int32_t _pad2;
     /* loudness geometry (pyloudnorm integrated_loudness, block 0.4 s, step 0.1 s) */
     int64_t n_blocks;
     const int64_t *block_lo; /* host [n_blocks] first frame of each block        */

@@ -9,6 +9,30 @@
 
 namespace mm {
 
+// Software-pipelined sequential stream: ld() yields the next element (called in
+// order), proc(v) consumes elements in order.  NB*B elements stay in flight in
+// registers, hiding HBM/Infinity-Cache latency behind a lane's dependent chain.
+template <int B, int NB, typename V, typename LD, typename PROC>
+__device__ __forceinline__ void stream(int len, LD &&ld, PROC &&proc) {
+    V buf[NB][B];
+#pragma unroll
+    for (int k = 0; k < NB; ++k)
+#pragma unroll
+        for (int j = 0; j < B; ++j)
+            if (k * B + j < len) buf[k][j] = ld();
+    for (int n0 = 0; n0 < len; n0 += NB * B) {
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+#pragma unroll
+            for (int j = 0; j < B; ++j)
+                if (n0 + k * B + j < len) proc(buf[k][j]);
+#pragma unroll
+            for (int j = 0; j < B; ++j)
+                if (n0 + (k + NB) * B + j < len) buf[k][j] = ld();
+        }
+    }
+}
+
 struct SatArgs {
     float keep, mix, drive;
     int on;
@@ -36,18 +60,21 @@ struct StageArgs {
 struct CompArgs {
     int64_t N_proc, G;
     int T, K, ch, warmup;
+    int S;                     // tiles per super-tile (envelope solve unit)
+    int64_t GS;                // super-tiles (chunks * ceil(K/S))
     const short2 *band[3];
     const double *max_att[3];  // device LUTs [32769]
     int look[3];
     double attack_frames[3], release_frames[3];
     double rcp_attack[3], rcp_release[3];
     double *M[3];              // tile-major per-frame max attenuation
-    double *start[3];          // per-tile start state
+    double *start[3];          // per-super-tile speculative start state
+    double *tstart[3];         // per-tile start state (recorded by the walks)
     const double *end_in[3];
     double *end_out[3];
     unsigned int *changed;
-    int32_t *ident[3];         // per tile: 1 if every frame has M == 0 (identity map)
-    int32_t *prev_active[3];   // per tile: nearest earlier non-identity tile in the chunk, -1 if none
+    int32_t *ident[3];         // per super-tile: 1 if every frame has M == 0 (identity map)
+    int32_t *prev_active[3];   // per super-tile: nearest earlier non-identity one in the chunk, -1 if none
     short2 *q_out;
 };
 

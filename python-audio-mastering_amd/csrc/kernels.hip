@@ -10,6 +10,11 @@
 // ingest.  Linear recurrences (EQ, crossover, K-weighting) use the two-pass block
 // method: pass 1 = zero-state end state per tile, a scan of affine state maps
 // across tiles (scan.hip), pass 2 = exact re-run from the carried state.
+//
+// Every per-lane walk is a software-pipelined stream (stream<> below): NB blocks
+// of B frames are in flight in registers while the recurrence consumes the
+// oldest block, which hides HBM/Infinity-Cache latency behind a single lane's
+// dependent f64 chain (there are only ~1-2 waves per SIMD at C2 sizes).
 #include "common.h"
 
 namespace mm {
@@ -48,10 +53,14 @@ __device__ __forceinline__ int16_t sat16(int32_t v) {
 // ---------------------------------------------------------------- biquads
 // DF2T section (scipy sosfilt / lfilter form): y = b0 x + z0;
 // z0 = b1 x - a1 y + z1; z1 = b2 x - a2 y.  State s = (z0, z1).
+// Written so that the y-independent halves (b1 x + z1, b2 x) sit off the
+// recurrence's critical path.
 __device__ __forceinline__ double df2t(double x, double &z0, double &z1, const double *c) {
     double y = fma(c[0], x, z0);
-    z0 = fma(c[1], x, fma(-c[3], y, z1));
-    z1 = fma(c[2], x, -c[4] * y);
+    double t0 = fma(c[1], x, z1);
+    double t1 = c[2] * x;
+    z0 = fma(-c[3], y, t0);
+    z1 = fma(-c[4], y, t1);
     return y;
 }
 
@@ -67,21 +76,10 @@ __device__ __forceinline__ double cascade(double x, double (&z)[NS][2], const do
 // (pydub pads a short final slice with silence).  Saturation f32, EQ cascade
 // f64 (each active AME stage is one sosfilt section; zero-gain stages are
 // dropped on the host), width f64, quantise -> q1 (tile-major short2).
-
-__device__ __forceinline__ void load_in(const float *in, int64_t f, int64_t N_in, int ch, float &l, float &r) {
-    if (f < N_in) {
-        if (ch == 2) {
-            float2 v = *reinterpret_cast<const float2 *>(in + 2 * f);
-            l = v.x;
-            r = v.y;
-        } else {
-            l = in[f];
-            r = 0.f;
-        }
-    } else {
-        l = 0.f;
-        r = 0.f;
-    }
+__device__ __forceinline__ float2 load_in(const float *in, int64_t f, int64_t N_in, int ch) {
+    if (f >= N_in) return make_float2(0.f, 0.f);
+    if (ch == 2) return *reinterpret_cast<const float2 *>(in + 2 * f);
+    return make_float2(in[f], 0.f);
 }
 
 template <int NS, bool PASS2>
@@ -111,28 +109,28 @@ __global__ void __launch_bounds__(256) eq_kernel(StageArgs a) {
         for (int k = 0; k < NS; ++k) zl[k][0] = zl[k][1] = zr[k][0] = zr[k][1] = 0.0;
     }
     const double(*sos)[5] = a.sos;
-    for (int n = 0; n < len; ++n) {
-        float l, r;
-        load_in(a.in, f0 + n, a.N_in, ch, l, r);
-        if (a.sat.on) {
-            l = saturate(l, a.sat);
-            r = saturate(r, a.sat);
-        }
-        double yl = cascade<NS>((double)l, zl, sos);
-        double yr = ch == 2 ? cascade<NS>((double)r, zr, sos) : 0.0;
-        if (PASS2) {
-            if (a.width_on) {  // apply_stereo_width (AME:136-144) in f64
-                double mid = (yl + yr) / 2;
-                double side = (yl - yr) / 2 * a.width;
-                yl = mid + side;
-                yr = mid - side;
+    int ln = 0, pn = 0;
+    stream<8, 3, float2>(
+        len, [&]() { return load_in(a.in, f0 + ln++, a.N_in, ch); },
+        [&](float2 v) {
+            float l = v.x, r = v.y;
+            if (a.sat.on) {
+                l = saturate(l, a.sat);
+                r = saturate(r, a.sat);
             }
-            short2 q;
-            q.x = quantize(yl);
-            q.y = quantize(yr);
-            a.q_out[(int64_t)n * a.G + g] = q;
-        }
-    }
+            double yl = cascade<NS>((double)l, zl, sos);
+            double yr = ch == 2 ? cascade<NS>((double)r, zr, sos) : 0.0;
+            if (PASS2) {
+                if (a.width_on) {  // apply_stereo_width (AME:136-144) in f64
+                    double mid = (yl + yr) / 2;
+                    double side = (yl - yr) / 2 * a.width;
+                    yl = mid + side;
+                    yr = mid - side;
+                }
+                a.q_out[(int64_t)pn * a.G + g] = make_short2(quantize(yl), quantize(yr));
+            }
+            ++pn;
+        });
     if (!PASS2) {
         double *z = a.z_out + (g * ch) * D;
 #pragma unroll
@@ -158,25 +156,26 @@ __global__ void __launch_bounds__(256) pre_pointwise_kernel(StageArgs a) {
     if (g >= a.G) return;
     const int64_t f0 = g * a.T;
     const int len = (int)min((int64_t)a.T, a.N_proc - f0);
-    for (int n = 0; n < len; ++n) {
-        float l, r;
-        load_in(a.in, f0 + n, a.N_in, a.ch, l, r);
-        if (a.sat.on) {
-            l = saturate(l, a.sat);
-            r = saturate(r, a.sat);
-        }
-        if (a.width_on) {
-            float w = (float)a.width;
-            float mid = __fdiv_rn(__fadd_rn(l, r), 2.0f);
-            float side = __fmul_rn(__fdiv_rn(__fsub_rn(l, r), 2.0f), w);
-            l = __fadd_rn(mid, side);
-            r = __fsub_rn(mid, side);
-        }
-        short2 q;
-        q.x = quantize((double)l);
-        q.y = a.ch == 2 ? quantize((double)r) : (int16_t)0;
-        a.q_out[(int64_t)n * a.G + g] = q;
-    }
+    int ln = 0, pn = 0;
+    stream<8, 2, float2>(
+        len, [&]() { return load_in(a.in, f0 + ln++, a.N_in, a.ch); },
+        [&](float2 v) {
+            float l = v.x, r = v.y;
+            if (a.sat.on) {
+                l = saturate(l, a.sat);
+                r = saturate(r, a.sat);
+            }
+            if (a.width_on) {
+                float w = (float)a.width;
+                float mid = __fdiv_rn(__fadd_rn(l, r), 2.0f);
+                float side = __fmul_rn(__fdiv_rn(__fsub_rn(l, r), 2.0f), w);
+                l = __fadd_rn(mid, side);
+                r = __fsub_rn(mid, side);
+            }
+            a.q_out[(int64_t)pn * a.G + g] =
+                make_short2(quantize((double)l), a.ch == 2 ? quantize((double)r) : (int16_t)0);
+            ++pn;
+        });
 }
 
 // ------------------------------------------------------ stage B: crossover
@@ -192,7 +191,9 @@ __global__ void __launch_bounds__(256) xover_kernel(StageArgs a) {
     const int ch = a.ch;
     constexpr int D = 8;
     double lo[2][2][2], hi[2][2][2];  // [channel][section][z]
+#pragma unroll
     for (int c = 0; c < 2; ++c)
+#pragma unroll
         for (int k = 0; k < 2; ++k) {
             if (PASS2 && c < ch) {
                 const double *s = a.s_in + (g * ch + c) * D;
@@ -205,35 +206,34 @@ __global__ void __launch_bounds__(256) xover_kernel(StageArgs a) {
             }
         }
     const double(*sos)[5] = a.sos;
-    for (int n = 0; n < len; ++n) {
-        const int64_t idx = (int64_t)n * a.G + g;
-        short2 q = a.q_in[idx];
-        double x[2] = {(double)((float)q.x / 32768.0f), (double)((float)q.y / 32768.0f)};
-        short2 qb[3];
-        int16_t *qbl = reinterpret_cast<int16_t *>(qb);
+    int ln = 0, pn = 0;
+    stream<8, 3, short2>(
+        len, [&]() { return a.q_in[(int64_t)(ln++) * a.G + g]; },
+        [&](short2 q) {
+            const double x[2] = {(double)((float)q.x / 32768.0f), (double)((float)q.y / 32768.0f)};
+            int32_t ob0[2] = {0, 0}, ob1[2] = {0, 0}, ob2[2] = {0, 0};
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            if (c >= ch) {
-                qbl[0 + c] = qbl[2 + c] = qbl[4 + c] = 0;
-                continue;
+            for (int c = 0; c < 2; ++c) {
+                if (c >= ch) break;
+                double yl = df2t(x[c], lo[c][0][0], lo[c][0][1], sos[0]);
+                yl = df2t(yl, lo[c][1][0], lo[c][1][1], sos[1]);
+                double yh = df2t(x[c], hi[c][0][0], hi[c][0][1], sos[2]);
+                yh = df2t(yh, hi[c][1][0], hi[c][1][1], sos[3]);
+                if (PASS2) {
+                    double ym = (x[c] - yl) - yh;
+                    ob0[c] = quantize(yl);
+                    ob1[c] = quantize(ym);
+                    ob2[c] = quantize(yh);
+                }
             }
-            double yl = df2t(x[c], lo[c][0][0], lo[c][0][1], sos[0]);
-            yl = df2t(yl, lo[c][1][0], lo[c][1][1], sos[1]);
-            double yh = df2t(x[c], hi[c][0][0], hi[c][0][1], sos[2]);
-            yh = df2t(yh, hi[c][1][0], hi[c][1][1], sos[3]);
             if (PASS2) {
-                double ym = (x[c] - yl) - yh;
-                qbl[0 + c] = quantize(yl);
-                qbl[2 + c] = quantize(ym);
-                qbl[4 + c] = quantize(yh);
+                const int64_t idx = (int64_t)pn * a.G + g;
+                a.band_out[0][idx] = make_short2((int16_t)ob0[0], (int16_t)ob0[1]);
+                a.band_out[1][idx] = make_short2((int16_t)ob1[0], (int16_t)ob1[1]);
+                a.band_out[2][idx] = make_short2((int16_t)ob2[0], (int16_t)ob2[1]);
             }
-        }
-        if (PASS2) {
-            a.band_out[0][idx] = qb[0];
-            a.band_out[1][idx] = qb[1];
-            a.band_out[2][idx] = qb[2];
-        }
-    }
+            ++pn;
+        });
     if (!PASS2) {
         for (int c = 0; c < ch; ++c) {
             double *z = a.z_out + (g * ch + c) * D;
@@ -251,23 +251,28 @@ __global__ void __launch_bounds__(256) xover_kernel(StageArgs a) {
 // pydub compress_dynamic_range per band (AME:207-209), restated in SURVEY.md
 // Appendix A.  rms over frames [max(chunk0, i-look), i) (excludes i), both
 // channels: audioop.rms = (unsigned)sqrt(S/n) which, for integer S and
-// n <= 2^12, equals isqrt(S div n) exactly (proved in DESIGN.md, checked in
-// tests).  Max attenuation M(rms) comes from a host table built with pydub's
-// own float expressions; inc/dec are M/attack_frames, M/release_frames
-// (correctly rounded).  'above' (rms > thresh) == (M != 0).
+// n <= 2^12, equals isqrt(S div n) exactly (tests/test_oracle.py).
+// Max attenuation M(rms) comes from a host table built with pydub's own float
+// expressions; inc/dec are M/attack_frames, M/release_frames (correctly
+// rounded).  'above' (rms > thresh) == (M != 0).
 
-__device__ __forceinline__ uint32_t rms_exact(int64_t S, int64_t n) {
+__device__ __forceinline__ int32_t frame_energy(short2 v) {
+    return (int32_t)v.x * v.x + (int32_t)v.y * v.y;
+}
+
+// largest r with n*r*r <= S (== trunc(sqrt(S/n)) computed in doubles)
+__device__ __forceinline__ uint32_t rms_exact(int64_t S, int64_t n, float inv_n) {
     if (n <= 0) return 0;
-    double q = (double)S / (double)n;
-    int64_t r = (int64_t)sqrt(q);
-    // integer fix-up: largest r with n*r*r <= S
+    int64_t r = (int64_t)__fsqrt_rn((float)S * inv_n);
     while (r > 0 && n * r * r > S) --r;
     while (n * (r + 1) * (r + 1) <= S) ++r;
     return (uint32_t)r;
 }
 
-__device__ __forceinline__ int32_t frame_energy(short2 v) {
-    return (int32_t)v.x * v.x + (int32_t)v.y * v.y;
+// tile-major address of timeline frame f
+__device__ __forceinline__ int64_t tm_index(int64_t f, int T, int64_t G) {
+    int64_t g = f / T;
+    return (f - g * T) * G + g;
 }
 
 // M[b][n*G+g] for every frame.  grid: (ceil(G/256), 3 bands)
@@ -278,35 +283,54 @@ __global__ void __launch_bounds__(256) comp_rms_kernel(CompArgs a) {
     const short2 *x = a.band[b];
     const double *lut = a.max_att[b];
     const int look = a.look[b];
-    const int64_t f0 = g * a.T;
-    const int64_t chunk0 = (g / a.K) * a.K * a.T;
-    const int len = (int)min((int64_t)a.T, a.N_proc - f0);
-    // initial window [max(chunk0, f0-look), f0)
-    int64_t lo = max(chunk0, f0 - look);
-    int64_t S = 0;
-    for (int64_t f = lo; f < f0; ++f) {
-        int64_t gg = f / a.T, nn = f - gg * a.T;
-        S += frame_energy(x[nn * a.G + gg]);
-    }
+    const int T = a.T;
+    const int64_t G = a.G;
+    const int64_t f0 = g * T;
+    const int64_t chunk0 = (g / a.K) * a.K * T;
+    const int len = (int)min((int64_t)T, a.N_proc - f0);
     const int ch = a.ch;
-    double *M = a.M[b];
-    for (int n = 0; n < len; ++n) {
-        const int64_t f = f0 + n;
-        const int64_t cnt = (f - lo) * ch;
-        uint32_t r = rms_exact(S, cnt);
-        M[(int64_t)n * a.G + g] = lut[r];
-        // slide: add frame f, drop frame f-look if it was in the window
-        S += frame_energy(x[(int64_t)n * a.G + g]);
-        int64_t drop = f - look;
-        if (drop >= lo) {
-            int64_t gg = drop / a.T, nn = drop - gg * a.T;
-            S -= frame_energy(x[nn * a.G + gg]);
-            lo = drop + 1;
-        }
+    // initial window [lo0, f0), lo0 = max(chunk0, f0 - look)
+    const int64_t lo0 = max(chunk0, f0 - look);
+    int64_t S = 0;
+    {
+        int64_t wf = lo0;
+        stream<8, 2, short2>(
+            (int)(f0 - lo0), [&]() { return x[tm_index(wf++, T, G)]; },
+            [&](short2 v) { S += frame_energy(v); });
     }
+    double *M = a.M[b];
+    int64_t cnt_frames = f0 - lo0;
+    float inv = cnt_frames > 0 ? 1.0f / (float)(cnt_frames * ch) : 0.f;
+    // two streams in lockstep: the new frame f and the dropped frame f - look
+    int64_t lf = f0, pf = f0;
+    struct Pair {
+        short2 in, drop;
+    };
+    stream<8, 3, Pair>(
+        len,
+        [&]() {
+            Pair p;
+            p.in = x[tm_index(lf, T, G)];
+            const int64_t fd = lf - look;
+            p.drop = fd >= chunk0 ? x[tm_index(fd, T, G)] : make_short2(0, 0);
+            ++lf;
+            return p;
+        },
+        [&](Pair p) {
+            const uint32_t r = rms_exact(S, cnt_frames * ch, inv);
+            M[(pf - f0) * G + g] = lut[r];
+            S += frame_energy(p.in);
+            if (pf - look >= chunk0) {
+                S -= frame_energy(p.drop);
+            } else {
+                ++cnt_frames;
+                inv = 1.0f / (float)(cnt_frames * ch);
+            }
+            ++pf;
+        });
 }
 
-// correctly rounded m / d given rd = RN(1/d) (Markstein)
+// correctly rounded m / d given rd = RN(1/d) (Markstein; tests/test_oracle.py)
 __device__ __forceinline__ double div_cr(double m, double d, double rd) {
     double q = m * rd;
     double rem = fma(-q, d, m);
@@ -318,16 +342,14 @@ struct BandStep {
 };
 
 __device__ __forceinline__ double comp_step(double att, double M, const BandStep &bs) {
-    if (M != 0.0 && att <= M) {
-        double inc = div_cr(M, bs.A, bs.rA);
-        att = att + inc;
-        att = (M < att) ? M : att;
-    } else {
-        double dec = div_cr(M, bs.R, bs.rR);
-        att = att - dec;
-        att = (0.0 > att) ? 0.0 : att;
-    }
-    return att;
+    // both candidates are computed off the att chain's critical path
+    const double inc = div_cr(M, bs.A, bs.rA);
+    const double dec = div_cr(M, bs.R, bs.rR);
+    double up = att + inc;
+    up = (M < up) ? M : up;
+    double dn = att - dec;
+    dn = (0.0 > dn) ? 0.0 : dn;
+    return (M != 0.0 && att <= M) ? up : dn;
 }
 
 __device__ __forceinline__ BandStep band_step(const CompArgs &a, int b) {
@@ -339,42 +361,93 @@ __device__ __forceinline__ BandStep band_step(const CompArgs &a, int b) {
     return s;
 }
 
-// Speculative pass: each (tile, band) starts from a warm-up run of W frames
-// (from 0) before its first frame; tile 0 of a chunk starts exactly at 0.
-// Also flags identity tiles (every frame has M == 0: att is held exactly).
-// grid: (ceil(G/256), 3)
-__global__ void __launch_bounds__(256) comp_pass0_kernel(CompArgs a) {
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int b = blockIdx.y;
-    if (g >= a.G) return;
-    const BandStep bs = band_step(a, b);
-    const double *M = a.M[b];
-    const int64_t f0 = g * a.T;
-    const int64_t chunk0 = (g / a.K) * a.K * a.T;
-    const int len = (int)min((int64_t)a.T, a.N_proc - f0);
-    double att = 0.0;
-    for (int64_t f = max(chunk0, f0 - a.warmup); f < f0; ++f) {
-        int64_t gg = f / a.T, nn = f - gg * a.T;
-        att = comp_step(att, M[nn * a.G + gg], bs);
+// A super-tile = up to S consecutive tiles of one chunk, the unit of the
+// speculative envelope solve (fewer, longer units -> fewer Jacobi sweeps).
+struct Super {
+    int64_t g0, g1;  // tiles [g0, g1)
+    int len;         // frames
+};
+
+__device__ __forceinline__ Super super_of(const CompArgs &a, int64_t s) {
+    const int64_t KS = (a.K + a.S - 1) / a.S;
+    const int64_t c = s / KS, k = s - c * KS;
+    Super r;
+    r.g0 = c * a.K + k * a.S;
+    r.g1 = min(min(r.g0 + a.S, (c + 1) * a.K), a.G);
+    if (r.g0 >= r.g1) {
+        r.len = 0;
+        r.g1 = r.g0;
+    } else {
+        r.len = (int)(min((int64_t)(r.g1) * a.T, a.N_proc) - r.g0 * a.T);
     }
-    a.start[b][g] = att;
-    int ident = 1;
-    for (int n = 0; n < len; ++n) {
-        double m = M[(int64_t)n * a.G + g];
-        ident &= (m == 0.0);
-        att = comp_step(att, m, bs);
-    }
-    a.end_out[b][g] = att;
-    a.ident[b][g] = ident;
+    return r;
 }
 
-// prev_active[g] = largest p < g in g's chunk with !ident[p], else -1.
+// Walk the envelope over a super-tile; optionally record the state at every
+// tile start (tstart) and report whether every frame had M == 0 (identity).
+template <bool RECORD>
+__device__ __forceinline__ double comp_walk(double att, const double *M, const CompArgs &a, const Super &st,
+                                            const BandStep &bs, double *tstart, int &ident) {
+    const int T = a.T;
+    const int64_t G = a.G;
+    int64_t lg = st.g0, pg = st.g0;
+    int ln = 0, pn = 0;
+    int id = 1;
+    stream<8, 4, double>(
+        st.len,
+        [&]() {
+            double v = M[(int64_t)ln * G + lg];
+            if (++ln == T) {
+                ln = 0;
+                ++lg;
+            }
+            return v;
+        },
+        [&](double m) {
+            if (RECORD && pn == 0) tstart[pg] = att;
+            id &= (m == 0.0);
+            att = comp_step(att, m, bs);
+            if (++pn == T) {
+                pn = 0;
+                ++pg;
+            }
+        });
+    ident = id;
+    return att;
+}
+
+// Speculative pass over super-tiles: each starts from a warm-up run over the
+// preceding super-tile of its chunk (from 0); the first super-tile of a chunk
+// starts exactly at 0.  Flags identity super-tiles (att held exactly).
+// grid: (ceil(GS/256), 3)
+__global__ void __launch_bounds__(256) comp_pass0_kernel(CompArgs a) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int b = blockIdx.y;
+    if (s >= a.GS) return;
+    const BandStep bs = band_step(a, b);
+    const double *M = a.M[b];
+    const Super st = super_of(a, s);
+    const int64_t KS = (a.K + a.S - 1) / a.S;
+    double att = 0.0;
+    int ident = 1;
+    if (a.warmup > 0 && (s % KS) != 0) {
+        const Super pv = super_of(a, s - 1);
+        att = comp_walk<false>(att, M, a, pv, bs, nullptr, ident);
+    }
+    a.start[b][s] = att;
+    att = comp_walk<true>(att, M, a, st, bs, a.tstart[b], ident);
+    a.end_out[b][s] = att;
+    a.ident[b][s] = st.len == 0 ? 1 : ident;
+}
+
+// prev_active[s] = largest p < s in s's chunk with !ident[p], else -1.
 // One 1024-thread block per (chunk, band): serial runs + Kogge-Stone max-scan.
 __global__ void __launch_bounds__(1024) comp_prev_active_kernel(CompArgs a) {
     __shared__ int64_t buf[1024];
     const int b = blockIdx.y;
-    const int64_t t0 = (int64_t)blockIdx.x * a.K;
-    const int64_t n = min((int64_t)a.K, a.G - t0);
+    const int64_t KS = (a.K + a.S - 1) / a.S;
+    const int64_t t0 = (int64_t)blockIdx.x * KS;
+    const int64_t n = min(KS, a.GS - t0);
     const int64_t c = (n + 1023) / 1024;
     const int tid = threadIdx.x;
     const int64_t b0 = tid * c, b1 = min(b0 + c, n);
@@ -398,78 +471,105 @@ __global__ void __launch_bounds__(1024) comp_prev_active_kernel(CompArgs a) {
     }
 }
 
-// One Jacobi sweep: an active tile whose start differs from the end of its
-// nearest active predecessor (identity tiles in between hold att exactly) is
-// re-run from that end.  Exact at convergence (every start == true state).
-__global__ void __launch_bounds__(256) comp_fix_kernel(CompArgs a) {
+// One Jacobi sweep: an active super-tile whose start differs from the end of
+// its nearest active predecessor (identity super-tiles in between hold att
+// exactly) is re-run from that end.  Exact at convergence (every start == true
+// state, by induction from the exact chunk start).  A sweep that follows a
+// sweep which changed nothing exits at once (converged), so the host queues
+// several per synchronisation.
+__global__ void __launch_bounds__(256) comp_fix_kernel(CompArgs a, const unsigned int *prev_changed) {
+    if (prev_changed && *prev_changed == 0u) return;
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int b = blockIdx.y;
+    if (s >= a.GS) return;
+    const double *end_in = a.end_in[b];
+    double e = end_in[s];
+    if (!a.ident[b][s]) {
+        const int32_t p = a.prev_active[b][s];
+        const double want = p >= 0 ? end_in[p] : 0.0;
+        const double have = a.start[b][s];
+        if (__double_as_longlong(want) != __double_as_longlong(have)) {
+            const BandStep bs = band_step(a, b);
+            const Super st = super_of(a, s);
+            int ident;
+            e = comp_walk<true>(want, a.M[b], a, st, bs, a.tstart[b], ident);
+            a.start[b][s] = want;
+            *a.changed = 1u;  // benign race: every writer stores 1
+        }
+    }
+    a.end_out[b][s] = e;
+}
+
+// Tile starts of identity super-tiles (att held == end of the nearest active
+// predecessor); active super-tiles already recorded theirs.  grid (ceil(G/256), 3)
+__global__ void __launch_bounds__(256) comp_hold_starts_kernel(CompArgs a) {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int b = blockIdx.y;
     if (g >= a.G) return;
-    const double *end_in = a.end_in[b];
-    double e = end_in[g];
-    if (!a.ident[b][g]) {
-        const int32_t p = a.prev_active[b][g];
-        double want = p >= 0 ? end_in[p] : 0.0;
-        double have = a.start[b][g];
-        if (__double_as_longlong(want) != __double_as_longlong(have)) {
-            const BandStep bs = band_step(a, b);
-            const double *M = a.M[b];
-            const int64_t f0 = g * a.T;
-            const int len = (int)min((int64_t)a.T, a.N_proc - f0);
-            double att = want;
-            for (int n = 0; n < len; ++n) att = comp_step(att, M[(int64_t)n * a.G + g], bs);
-            a.start[b][g] = want;
-            e = att;
-            atomicAdd(a.changed, 1u);
-        }
+    const int64_t KS = (a.K + a.S - 1) / a.S;
+    const int64_t c = g / a.K;
+    const int64_t s = c * KS + (g - c * a.K) / a.S;
+    if (a.ident[b][s]) {
+        const int32_t p = a.prev_active[b][s];
+        a.tstart[b][g] = p >= 0 ? a.end_in[b][p] : 0.0;
     }
-    a.end_out[b][g] = e;
 }
 
-// Final pass: exact trajectory from the converged starts; gains applied to the
-// three band samples (audioop.mul floor), overlay sat16(sat16(lo+mid)+hi)
-// (AME:210) -> q2.
+// Final pass per tile: exact trajectory from the converged tile starts; gains
+// applied to the three band samples (audioop.mul floor), overlay
+// sat16(sat16(lo+mid)+hi) (AME:210) -> q2.
 __global__ void __launch_bounds__(256) comp_apply_kernel(CompArgs a) {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= a.G) return;
     BandStep bs[3];
     double att[3];
+#pragma unroll
     for (int b = 0; b < 3; ++b) {
         bs[b] = band_step(a, b);
-        if (a.ident[b][g]) {  // held tile: att == end of the nearest active predecessor
-            const int32_t p = a.prev_active[b][g];
-            att[b] = p >= 0 ? a.end_in[b][p] : 0.0;
-        } else {
-            att[b] = a.start[b][g];
-        }
+        att[b] = a.tstart[b][g];
     }
+    const int64_t G = a.G;
     const int64_t f0 = g * a.T;
     const int len = (int)min((int64_t)a.T, a.N_proc - f0);
-    for (int n = 0; n < len; ++n) {
-        const int64_t idx = (int64_t)n * a.G + g;
-        int32_t accl = 0, accr = 0;
+    struct Fr {
+        double m[3];
+        short2 v[3];
+    };
+    int ln = 0, pn = 0;
+    stream<4, 2, Fr>(
+        len,
+        [&]() {
+            Fr f;
+            const int64_t idx = (int64_t)(ln++) * G + g;
 #pragma unroll
-        for (int b = 0; b < 3; ++b) {
-            att[b] = comp_step(att[b], a.M[b][idx], bs[b]);
-            short2 v = a.band[b][idx];
-            if (att[b] != 0.0) {
-                double gain = exp10(-att[b] / 20.0);
-                v.x = audioop_mul(v.x, gain);
-                v.y = audioop_mul(v.y, gain);
+            for (int b = 0; b < 3; ++b) {
+                f.m[b] = a.M[b][idx];
+                f.v[b] = a.band[b][idx];
             }
-            if (b == 0) {
-                accl = v.x;
-                accr = v.y;
-            } else {
-                accl = sat16(accl + v.x);
-                accr = sat16(accr + v.y);
+            return f;
+        },
+        [&](const Fr &f) {
+            int32_t accl = 0, accr = 0;
+#pragma unroll
+            for (int b = 0; b < 3; ++b) {
+                att[b] = comp_step(att[b], f.m[b], bs[b]);
+                short2 s = f.v[b];
+                if (att[b] != 0.0) {
+                    const double gain = exp10(-att[b] / 20.0);
+                    s.x = audioop_mul(s.x, gain);
+                    s.y = audioop_mul(s.y, gain);
+                }
+                if (b == 0) {
+                    accl = s.x;
+                    accr = s.y;
+                } else {
+                    accl = sat16(accl + s.x);
+                    accr = sat16(accr + s.y);
+                }
             }
-        }
-        short2 o;
-        o.x = (int16_t)accl;
-        o.y = a.ch == 2 ? (int16_t)accr : (int16_t)0;
-        a.q_out[idx] = o;
-    }
+            a.q_out[(int64_t)(pn++) * G + g] =
+                make_short2((int16_t)accl, a.ch == 2 ? (int16_t)accr : (int16_t)0);
+        });
 }
 
 // ------------------------------------------------- stage D: K-weighting
@@ -497,8 +597,7 @@ __global__ void __launch_bounds__(256) kweight_kernel(KwArgs a) {
     // segment bookkeeping
     int64_t seg = 0, seg_end = 0;
     if (PASS2) {
-        // largest s with bounds[s] <= f0
-        int64_t lo = 0, hi = a.n_segs;  // bounds has n_segs+1 entries
+        int64_t lo = 0, hi = a.n_segs;  // largest s with bounds[s] <= f0
         while (hi - lo > 1) {
             int64_t mid = (lo + hi) >> 1;
             if (a.seg_bounds[mid] <= f0) lo = mid;
@@ -508,24 +607,23 @@ __global__ void __launch_bounds__(256) kweight_kernel(KwArgs a) {
         seg_end = a.seg_bounds[seg + 1];
     }
     double e0 = 0.0, e1 = 0.0;
-    bool second = false;
-    for (int n = 0; n < len; ++n) {
-        short2 q = a.mix[(int64_t)n * a.G + g];
-        float m = a.ch == 2 ? ((float)q.x + (float)q.y) * (1.0f / 65536.0f) : (float)q.x * (1.0f / 32768.0f);
-        double y1 = df2t((double)m, z[0][0], z[0][1], a.sos[0]);
-        float y1f = (float)y1;
-        double y2 = df2t((double)y1f, z[1][0], z[1][1], a.sos[1]);
-        if (PASS2) {
-            float y2f = (float)y2;
-            double e = (double)y2f * (double)y2f;
-            if (f0 + n >= seg_end) {
-                second = true;
-                seg_end = 0x7fffffffffffffffLL;
+    int64_t pf = f0;
+    int ln = 0;
+    stream<8, 3, short2>(
+        len, [&]() { return a.mix[(int64_t)(ln++) * a.G + g]; },
+        [&](short2 q) {
+            float m = a.ch == 2 ? ((float)q.x + (float)q.y) * (1.0f / 65536.0f) : (float)q.x * (1.0f / 32768.0f);
+            double y1 = df2t((double)m, z[0][0], z[0][1], a.sos[0]);
+            float y1f = (float)y1;
+            double y2 = df2t((double)y1f, z[1][0], z[1][1], a.sos[1]);
+            if (PASS2) {
+                float y2f = (float)y2;
+                double e = (double)y2f * (double)y2f;
+                if (pf < seg_end) e0 += e;
+                else e1 += e;
             }
-            if (second) e1 += e;
-            else e0 += e;
-        }
-    }
+            ++pf;
+        });
     if (PASS2) {
         a.part[2 * g] = e0;
         a.part[2 * g + 1] = e1;
@@ -560,9 +658,9 @@ __global__ void seg_reduce_kernel(KwArgs a, double *seg_energy) {
 // AME:84-89: y = int16/32768 (f32); with a loudness target the gain is an
 // np.float64 so y*gain, the soft limiter and the clip run in f64; without
 // one they run in f32.  Output natural interleaved layout.  A block handles
-// 64 tiles: the tile-major mix is read coalesced into LDS, then written out
-// frame-major coalesced.
-constexpr int FIN_TILES = 64;
+// FIN_TILES tiles: the tile-major mix is read coalesced into LDS, then written
+// out frame-major coalesced.
+constexpr int FIN_TILES = 32;
 
 __device__ __forceinline__ double limiter64(double y) {
     double ay = fabs(y);
@@ -596,7 +694,6 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
     const int stride = T + 1;
     const int64_t g0 = (int64_t)blockIdx.x * FIN_TILES;
     const int ntile = (int)min((int64_t)FIN_TILES, a.G - g0);
-    // load: row n, lanes over tiles
     for (int i = threadIdx.x; i < T * FIN_TILES; i += blockDim.x) {
         int n = i / FIN_TILES, t = i - n * FIN_TILES;
         if (t < ntile) lds[t * stride + n] = a.mix[(int64_t)n * a.G + g0 + t];
@@ -608,7 +705,7 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
         int t = (int)(i / T), n = (int)(i - (int64_t)t * T);
         short2 q = lds[t * stride + n];
         int16_t o[2];
-        int16_t qq[2] = {q.x, q.y};
+        const int16_t qq[2] = {q.x, q.y};
         for (int c = 0; c < a.ch; ++c) {
             float y = (float)qq[c] / 32768.0f;
             if (a.use_gain) {

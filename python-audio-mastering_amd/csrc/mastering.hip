@@ -290,19 +290,25 @@ static int stage_chunks(mm_ctx *c, const mm_job *j, const float *d_in) {
         ca.K = K;
         ca.ch = ch;
         ca.warmup = j->comp_warmup;
+        ca.S = std::max(1, j->comp_super);
+        const int64_t KS = (K + ca.S - 1) / ca.S;
+        const int64_t nchunks = (G + K - 1) / K;
+        ca.GS = nchunks * KS;
+        const int64_t GS = ca.GS;
         short2 *q2;
         RET(get_buf(c, "q2", TG, &q2));
         ca.q_out = q2;
-        double *st, *eA, *eB, *luts;
-        RET(get_buf(c, "comp_start", (size_t)3 * G, &st));
-        RET(get_buf(c, "comp_endA", (size_t)3 * G, &eA));
-        RET(get_buf(c, "comp_endB", (size_t)3 * G, &eB));
+        double *st, *eA, *eB, *luts, *tst;
+        RET(get_buf(c, "comp_start", (size_t)3 * GS, &st));
+        RET(get_buf(c, "comp_endA", (size_t)3 * GS, &eA));
+        RET(get_buf(c, "comp_endB", (size_t)3 * GS, &eB));
+        RET(get_buf(c, "comp_tstart", (size_t)3 * G, &tst));
         RET(get_buf(c, "comp_lut", (size_t)3 * 32769, &luts));
         unsigned int *changed;
         RET(get_buf(c, "comp_changed", 64, &changed));
         int32_t *ident, *prev;
-        RET(get_buf(c, "comp_ident", (size_t)3 * G, &ident));
-        RET(get_buf(c, "comp_prev", (size_t)3 * G, &prev));
+        RET(get_buf(c, "comp_ident", (size_t)3 * GS, &ident));
+        RET(get_buf(c, "comp_prev", (size_t)3 * GS, &prev));
         for (int b = 0; b < 3; ++b) {
             double *Mb;
             char nm[16];
@@ -318,17 +324,19 @@ static int stage_chunks(mm_ctx *c, const mm_job *j, const float *d_in) {
             ca.release_frames[b] = j->band[b].release_frames;
             ca.rcp_attack[b] = 1.0 / j->band[b].attack_frames;
             ca.rcp_release[b] = 1.0 / j->band[b].release_frames;
-            ca.start[b] = st + (size_t)b * G;
-            ca.ident[b] = ident + (size_t)b * G;
-            ca.prev_active[b] = prev + (size_t)b * G;
-            ca.end_out[b] = eA + (size_t)b * G;
+            ca.start[b] = st + (size_t)b * GS;
+            ca.tstart[b] = tst + (size_t)b * G;
+            ca.ident[b] = ident + (size_t)b * GS;
+            ca.prev_active[b] = prev + (size_t)b * GS;
+            ca.end_out[b] = eA + (size_t)b * GS;
         }
+        const unsigned nbs = blocks_for(GS, 256);
         RET(launch(c, "comp_rms", comp_rms_kernel, dim3(nb, 3), dim3(256), 0, ca));
-        RET(launch(c, "comp_pass0", comp_pass0_kernel, dim3(nb, 3), dim3(256), 0, ca));
-        const unsigned nchunks = (unsigned)((G + K - 1) / K);
-        RET(launch(c, "comp_prev_active", comp_prev_active_kernel, dim3(nchunks, 3), dim3(1024), 0, ca));
-        // Jacobi sweeps in batches; stop when a sweep changed nothing.
-        const int batch = 4;
+        RET(launch(c, "comp_pass0", comp_pass0_kernel, dim3(nbs, 3), dim3(256), 0, ca));
+        RET(launch(c, "comp_prev_active", comp_prev_active_kernel, dim3((unsigned)nchunks, 3), dim3(1024), 0, ca));
+        // Jacobi sweeps queued in batches: sweep k writes flag k, and exits at once
+        // if sweep k-1 changed nothing; one host sync per batch.
+        const int batch = 16;
         int iters = 0;
         double *cur = eA, *nxt = eB;
         bool done = false;
@@ -336,11 +344,12 @@ static int stage_chunks(mm_ctx *c, const mm_job *j, const float *d_in) {
             HIPCHK(c, hipMemsetAsync(changed, 0, batch * sizeof(unsigned int), c->stream));
             for (int k = 0; k < batch; ++k) {
                 for (int b = 0; b < 3; ++b) {
-                    ca.end_in[b] = cur + (size_t)b * G;
-                    ca.end_out[b] = nxt + (size_t)b * G;
+                    ca.end_in[b] = cur + (size_t)b * GS;
+                    ca.end_out[b] = nxt + (size_t)b * GS;
                 }
                 ca.changed = changed + k;
-                RET(launch(c, "comp_fix", comp_fix_kernel, dim3(nb, 3), dim3(256), 0, ca));
+                const unsigned int *prevf = k > 0 ? changed + (k - 1) : nullptr;
+                RET(launch(c, "comp_fix", comp_fix_kernel, dim3(nbs, 3), dim3(256), 0, ca, prevf));
                 std::swap(cur, nxt);
             }
             unsigned int h[batch];
@@ -348,6 +357,8 @@ static int stage_chunks(mm_ctx *c, const mm_job *j, const float *d_in) {
             HIPCHK(c, hipStreamSynchronize(c->stream));
             for (int k = 0; k < batch; ++k) {
                 if (h[k] == 0) {
+                    // sweep k changed nothing, so it copied end_in to end_out and
+                    // both buffers hold the converged ends; later sweeps exited early.
                     done = true;
                     break;
                 }
@@ -357,7 +368,8 @@ static int stage_chunks(mm_ctx *c, const mm_job *j, const float *d_in) {
                 return set_err(c, MM_ERR_STATE, "compressor did not converge in %d sweeps", iters);
         }
         c->job.comp_max_iters = iters;  // reported via mm_result
-        for (int b = 0; b < 3; ++b) ca.end_in[b] = cur + (size_t)b * G;  // converged ends
+        for (int b = 0; b < 3; ++b) ca.end_in[b] = cur + (size_t)b * GS;  // converged ends
+        RET(launch(c, "comp_hold_starts", comp_hold_starts_kernel, dim3(nb, 3), dim3(256), 0, ca));
         RET(launch(c, "comp_apply", comp_apply_kernel, dim3(nb), dim3(256), 0, ca));
         mix = q2;
     } else {

@@ -27,7 +27,7 @@ MAX_DIM = 8
 SCAN_POWERS = 12
 SCAN_THREADS = 1024
 CHUNK_MS = 30 * 1000  # AME:48
-DEFAULT_TILE = 250     # divides 30 s chunks at every rate that is a multiple of 25 Hz
+DEFAULT_TILE = 125     # divides 30 s chunks at every rate that is a multiple of 25 Hz
 
 EQ_KEYS = ("bass_boost", "mid_cut", "presence_boost", "treble_boost")
 BAND_TIMES = ((10.0, 200.0), (5.0, 150.0), (1.0, 50.0))  # (attack, release) ms, AME:207-209

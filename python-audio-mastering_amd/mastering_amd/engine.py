@@ -28,8 +28,9 @@ EQ_PRESETS = {
              "description": "Warm low-mids for guitars and punchy presence for snare/vocals."},
 }
 
-COMP_WARMUP = 250
+COMP_WARMUP = 1          # warm up each super-tile over its predecessor
 COMP_MAX_ITERS = 100000
+COMP_SUPER_FRAMES = 1000  # envelope solve unit (frames) -> ~8 Jacobi sweeps on pink noise
 
 
 class Job:
@@ -96,6 +97,7 @@ class Job:
                 jb.max_att = tab.ctypes.data_as(native.c_double_p)
         j.comp_warmup = COMP_WARMUP
         j.comp_max_iters = COMP_MAX_ITERS
+        j.comp_super = max(1, round(COMP_SUPER_FRAMES / self.tile))
         # --- loudness
         if lufs is not None:
             self._fill_iir(j.kweight, design.kweight_sections(self.rate), [2], max(G, 1), self.tile, last_len)

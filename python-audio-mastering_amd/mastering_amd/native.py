@@ -43,6 +43,7 @@ class MMJob(ctypes.Structure):
                 ("multiband_on", ctypes.c_int32), ("lufs_on", ctypes.c_int32), ("out_kind", ctypes.c_int32),
                 ("lufs_target", ctypes.c_double), ("eq", MMIir), ("xover", MMIir), ("kweight", MMIir),
                 ("band", MMBand * 3), ("comp_warmup", ctypes.c_int32), ("comp_max_iters", ctypes.c_int32),
+                ("comp_super", ctypes.c_int32), ("_pad2", ctypes.c_int32),
                 ("n_blocks", ctypes.c_int64), ("block_lo", c_int64_p), ("block_hi", c_int64_p),
                 ("n_segs", ctypes.c_int64), ("seg_bounds", c_int64_p), ("block_scale", ctypes.c_double)]
 
@@ -68,6 +69,10 @@ def load():
     with _lock:
         if _lib is not None:
             return _lib
+        try:  # share ONE HIP runtime with PyTorch when it is present (same soname)
+            import torch  # noqa: F401
+        except Exception:
+            pass
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"HIP extension not built: {LIB_PATH} missing (run __graft_entry__.build())")
         lib = ctypes.CDLL(LIB_PATH)

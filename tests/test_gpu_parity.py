@@ -58,27 +58,46 @@ def test_vs_oracle(oracle, seconds, params, track):
     _check(out, info, ref, L)
 
 
-def test_mix_bit_exact(oracle):
-    """Pre-gain mix (chunks + multiband + overlay, AME:48-80) is integer work: bit-exact
-    up to IIR last-bit effects; we require >= 99.999 % identical samples."""
-    from mastering_amd.synth import pink_noise_pcm16
-    from mastering_amd import Job, native
+def _staged_mix(pcm, params):
     import ctypes
-    pcm = pink_noise_pcm16(31 * 44100, 44100, 2, 5)
-    job = Job(pcm.shape[0], 44100, 2, P_HOT)
-    ctx = native.context(0)
-    x = np.ascontiguousarray(pcm.astype(np.float32) / 32768)
+
     import torch
-    d_in = torch.from_numpy(x).cuda()
+
+    from mastering_amd import Job, native
+    job = Job(pcm.shape[0], 44100, 2, params)
+    ctx = native.context(0)
+    d_in = torch.from_numpy(np.ascontiguousarray(pcm.astype(np.float32) / 32768)).cuda()
     ctx.check(ctx.lib.mm_stage_chunks(ctx.ptr, ctypes.byref(job.job), ctypes.c_void_p(d_in.data_ptr())), "stage")
     mix = np.empty((job.frames_proc, 2), np.int16)
     ctx.check(ctx.lib.mm_read_mix(ctx.ptr, mix.ctypes.data_as(ctypes.POINTER(ctypes.c_int16))), "read_mix")
-    # oracle mix
+    return mix
+
+
+def _oracle_mix(oracle, pcm, params):
+    thr, rat = oracle.multiband_params(params)
     ref = []
-    thr, rat = oracle.multiband_params(P_HOT)
     for s, e in oracle.chunk_ranges(pcm.shape[0], 44100):
-        c = pcm[s:e]
-        y = oracle.quantize(oracle.stereo_width(oracle.equalize(oracle.saturation(oracle.pcm_to_float(c), 30), 44100, P_HOT), 1.3))
+        x = oracle.saturation(oracle.pcm_to_float(pcm[s:e]), params.get("saturation", 0))
+        y = oracle.quantize(oracle.stereo_width(oracle.equalize(x, 44100, params), params.get("width", 1.0)))
         ref.append(oracle.multiband(y, 44100, thr, rat))
-    ref = np.concatenate(ref)
-    assert np.mean(mix == ref) >= 0.99999, np.mean(mix == ref)
+    return np.concatenate(ref)
+
+
+def test_mix_bit_exact_without_tanh(oracle):
+    """Pre-gain mix (chunks + EQ + width + multiband + overlay, AME:48-80) with the
+    exciter off: everything left is f64 IIR (tile-scan carries differ from scipy in the
+    last bits only) and integer work, so >= 99.9999 % of samples must be identical."""
+    from mastering_amd.synth import pink_noise_pcm16
+    params = dict(P_HOT, saturation=0)
+    pcm = pink_noise_pcm16(31 * 44100, 44100, 2, 5)
+    mix, ref = _staged_mix(pcm, params), _oracle_mix(oracle, pcm, params)
+    assert np.mean(mix == ref) >= 0.999999, np.mean(mix == ref)
+
+
+def test_mix_with_exciter(oracle):
+    """With the exciter on, numpy's float32 tanh is not correctly rounded (1 ulp apart from
+    the GPU's tanhf on ~30 % of samples), which flips a few int16 truncations: tolerance."""
+    from mastering_amd.synth import pink_noise_pcm16
+    pcm = pink_noise_pcm16(31 * 44100, 44100, 2, 5)
+    mix, ref = _staged_mix(pcm, P_HOT), _oracle_mix(oracle, pcm, P_HOT)
+    assert rms_diff(mix, ref) <= RMS_TOL and np.mean(mix == ref) >= 0.999
