@@ -43,18 +43,23 @@ typedef struct mm_ctx mm_ctx;
 
 /* One IIR stage = 1..2 branches of cascaded DF2T biquads fed by the same input.
  * sos[s] = {b0, b1, b2, a1, a2} (a0 == 1), branches laid out branch-major.
- * phi/phi_pow/phi_last: state-transition matrices (row-major MM_MAX_DIM x
- * MM_MAX_DIM, only dim x dim used) of the zero-input recurrence over one tile
- * (phi), over c*2^k tiles (phi_pow[k], c = tiles per scan thread) and over the
- * last (possibly partial) tile of a line (phi_last). */
+ * State-transition matrices (row-major MM_MAX_DIM x MM_MAX_DIM, only dim x dim
+ * used) of the zero-input recurrence, for the three-level tile scan:
+ *   phi          one tile (A^T)
+ *   phi_pow[k]   2^k tiles                          (block-local scan, k < 8)
+ *   phi_blk      one block of 256 tiles
+ *   phi_blk_pow[k]  256*c*2^k tiles, c = blocks per thread of the block scan
+ *   phi_last     the last (possibly partial) tile of the track */
 typedef struct mm_iir {
     int32_t nsec;            /* total sections (0 = stage inactive)           */
     int32_t nsec_branch0;    /* sections in branch 0 (rest are branch 1)      */
     int32_t dim;             /* state dim per channel = 2 * nsec              */
-    int32_t scan_c;          /* tiles per scan thread the powers were made for */
+    int32_t scan_c;          /* blocks per thread the block powers were made for */
     double sos[4][5];
     double phi[MM_MAX_DIM * MM_MAX_DIM];
     double phi_pow[MM_SCAN_POWERS][MM_MAX_DIM * MM_MAX_DIM];
+    double phi_blk[MM_MAX_DIM * MM_MAX_DIM];
+    double phi_blk_pow[MM_SCAN_POWERS][MM_MAX_DIM * MM_MAX_DIM];
     double phi_last[MM_MAX_DIM * MM_MAX_DIM];
 } mm_iir;
 
@@ -64,8 +69,10 @@ typedef struct mm_band {
     double attack_frames;    /* attack_ms * (rate/1000.0)                      */
     double release_frames;   /* release_ms * (rate/1000.0)                     */
     int32_t look;            /* int(attack_frames)                             */
-    int32_t _pad;
-    const double *max_att;   /* host table [32769]: max attenuation for rms r  */
+    int32_t r0;              /* smallest rms r with max_att[r] != 0 (32769: none) */
+    const double *max_att;   /* host table [32769]: max attenuation for rms r;
+                                immutable while the context holds it (uploaded
+                                once per distinct pointer)                     */
 } mm_band;
 
 /* A mastering job for one track (geometry + settings, all host memory). */
@@ -93,7 +100,7 @@ typedef struct mm_job {
     mm_band band[3];         /* low / mid / high                                */
     int32_t comp_warmup;     /* >0: speculative warm-up over the previous super-tile */
     int32_t comp_max_iters;  /* cap on fix-up sweeps (exactness check)          */
-    int32_t comp_super;      /* tiles per super-tile of the envelope solve      */
+    int32_t comp_super;      /* active frames per super-tile of the envelope solve */
     int32_t _pad2;
     /* loudness geometry (pyloudnorm integrated_loudness, block 0.4 s, step 0.1 s) */
     int64_t n_blocks;

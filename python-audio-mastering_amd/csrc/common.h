@@ -9,27 +9,98 @@
 
 namespace mm {
 
-// Software-pipelined sequential stream: ld() yields the next element (called in
-// order), proc(v) consumes elements in order.  NB*B elements stay in flight in
-// registers, hiding HBM/Infinity-Cache latency behind a lane's dependent chain.
+// Software-pipelined sequential stream over elements 0..len-1: ld(i) returns
+// element i and MUST be safe (clamped) for any i < len + NB*B; proc(v) consumes
+// elements in order.  NB*B elements stay in flight in registers, hiding
+// HBM/Infinity-Cache latency behind a lane's dependent chain.  The main loop is
+// branch-free (no conditional loads or stores), which lets the compiler use
+// counted s_waitcnt vmcnt(N) instead of draining every load; the ragged tail
+// is consumed once after it.
 template <int B, int NB, typename V, typename LD, typename PROC>
 __device__ __forceinline__ void stream(int len, LD &&ld, PROC &&proc) {
+    constexpr int R = B * NB;
+    if (len <= 0) return;
+    // sched_barrier pins the issue order of the load blocks to be the same in
+    // the prologue and in the loop body; without it the scheduler permutes the
+    // prologue loads, the two paths into the loop header disagree on which
+    // register is oldest, and the waitcnt pass falls back to vmcnt(0).
     V buf[NB][B];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+#pragma unroll
+        for (int j = 0; j < B; ++j) buf[k][j] = ld(k * B + j);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    const int nfull = len / R;
+    int base = 0;
+    for (int r = 0; r < nfull; ++r, base += R) {
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+#pragma unroll
+            for (int j = 0; j < B; ++j) proc(buf[k][j]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < B; ++j) buf[k][j] = ld(base + R + k * B + j);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    const int rem = len - base;
 #pragma unroll
     for (int k = 0; k < NB; ++k)
 #pragma unroll
         for (int j = 0; j < B; ++j)
-            if (k * B + j < len) buf[k][j] = ld();
-    for (int n0 = 0; n0 < len; n0 += NB * B) {
+            if (k * B + j < rem) proc(buf[k][j]);
+}
+
+// Two-stage variant for dependent gathers: ld1(i) is streamed NB blocks ahead,
+// ld2(v1) (e.g. a table lookup indexed by the loaded value) is issued one block
+// ahead of its use, so both latencies hide behind the consumer proc(v1, v2).
+// ld2 must be safe for any v1 that ld1 can return.
+template <int B, int NB, typename V1, typename V2, typename LD1, typename LD2, typename PROC>
+__device__ __forceinline__ void stream2(int len, LD1 &&ld1, LD2 &&ld2, PROC &&proc) {
+    constexpr int R = B * NB;
+    if (len <= 0) return;
+    V1 a[NB][B];
+    V2 m[B];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+#pragma unroll
+        for (int j = 0; j < B; ++j) a[k][j] = ld1(k * B + j);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int j = 0; j < B; ++j) m[j] = ld2(a[0][j]);
+    __builtin_amdgcn_sched_barrier(0);
+    const int nfull = len / R;
+    int base = 0;
+    for (int r = 0; r < nfull; ++r, base += R) {
 #pragma unroll
         for (int k = 0; k < NB; ++k) {
+            V2 mn[B];
 #pragma unroll
-            for (int j = 0; j < B; ++j)
-                if (n0 + k * B + j < len) proc(buf[k][j]);
+            for (int j = 0; j < B; ++j) mn[j] = ld2(a[(k + 1) % NB][j]);
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int j = 0; j < B; ++j)
-                if (n0 + (k + NB) * B + j < len) buf[k][j] = ld();
+            for (int j = 0; j < B; ++j) proc(a[k][j], m[j]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < B; ++j) a[k][j] = ld1(base + R + k * B + j);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < B; ++j) m[j] = mn[j];
         }
+    }
+    const int rem = len - base;
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+        V2 mn[B];
+#pragma unroll
+        for (int j = 0; j < B; ++j) mn[j] = ld2(a[(k + 1) % NB][j]);
+#pragma unroll
+        for (int j = 0; j < B; ++j)
+            if (k * B + j < rem) proc(a[k][j], m[j]);
+#pragma unroll
+        for (int j = 0; j < B; ++j) m[j] = mn[j];
     }
 }
 
@@ -60,21 +131,25 @@ struct StageArgs {
 struct CompArgs {
     int64_t N_proc, G;
     int T, K, ch, warmup;
-    int S;                     // tiles per super-tile (envelope solve unit)
-    int64_t GS;                // super-tiles (chunks * ceil(K/S))
+    int U;                     // active frames per super-tile (envelope solve unit)
+    int64_t SPC;               // super-tiles reserved per chunk = ceil(chunk frames / U)
+    int64_t GS;                // super-tiles = chunks * SPC
     const short2 *band[3];
     const double *max_att[3];  // device LUTs [32769]
+    uint32_t r0[3];            // smallest rms with max_att != 0 ("above threshold")
     int look[3];
     double attack_frames[3], release_frames[3];
     double rcp_attack[3], rcp_release[3];
-    double *M[3];              // tile-major per-frame max attenuation
+    uint16_t *r16[3];          // tile-major audioop.rms per frame
+    int32_t *cnt[3];           // per tile: active frames
+    int32_t *off[3];           // per tile: compacted index of its first active frame (in chunk)
+    int32_t *total[3];         // per chunk: active frames
+    double *Mc[3];             // compacted max attenuation, super-tile-major [U][GS]
     double *start[3];          // per-super-tile speculative start state
     double *tstart[3];         // per-tile start state (recorded by the walks)
     const double *end_in[3];
     double *end_out[3];
     unsigned int *changed;
-    int32_t *ident[3];         // per super-tile: 1 if every frame has M == 0 (identity map)
-    int32_t *prev_active[3];   // per super-tile: nearest earlier non-identity one in the chunk, -1 if none
     short2 *q_out;
 };
 
@@ -99,20 +174,23 @@ struct FinArgs {
     void *out;
 };
 
-// Affine state scan over tiles of independent lines (chunks x channels).
+// Segmented affine state scan over the tiles of a track (scan.hip).
 struct ScanArgs {
-    int dim;            // state dim per channel (<= 8)
-    int c;              // tiles per thread
-    int ch;             // channels interleaved in z: [tile][ch][dim]
-    int64_t line_tiles; // tiles per line (last line may be shorter)
-    int64_t G;          // total tiles
-    const double *phi;      // [8*8]  one tile
-    const double *phi_pow;  // [MM_SCAN_POWERS][8*8]  Phi^(c*2^k)
-    const double *phi_last; // [8*8]  last tile of a line
-    const double *z;        // per-tile zero-state end state
-    double *s;              // per-tile carry-in state (exclusive prefix)
-    const double *init;     // optional per-line initial state [lines][ch][dim] (or null)
-    double *line_end;       // optional per-line end state [lines][ch][dim] (or null)
+    int dim;            // state stride per channel (4 or 8)
+    int ch;             // channels interleaved in z/s: [tile][ch][dim]
+    int64_t line_tiles; // state resets to 0 at tiles g % line_tiles == 0
+    int64_t G;          // tiles
+    int64_t nblk;       // blocks of 256 tiles
+    int64_t c;          // blocks per thread in the block scan
+    const double *mats; // device: phi, pow2[12], blk, blk_pow[12], last (8x8 each)
+    const double *z;    // per-tile zero-state end state
+    double *s;          // per-tile carry-in state (output)
+    uint8_t *need;      // [G][ch] tile needs the block carry
+    double *agg;        // [nblk][ch][dim] block aggregates
+    int *agg_f;         // [nblk][ch] reset inside block
+    double *carry;      // [nblk][ch][dim] state at each block start
+    const double *init; // optional state at the track start [ch][dim] (or null)
+    double *line_end;   // optional state after the last tile [ch][dim] (or null)
 };
 
 }  // namespace mm

@@ -76,19 +76,23 @@ __device__ __forceinline__ double cascade(double x, double (&z)[NS][2], const do
 // (pydub pads a short final slice with silence).  Saturation f32, EQ cascade
 // f64 (each active AME stage is one sosfilt section; zero-gain stages are
 // dropped on the host), width f64, quantise -> q1 (tile-major short2).
-__device__ __forceinline__ float2 load_in(const float *in, int64_t f, int64_t N_in, int ch) {
-    if (f >= N_in) return make_float2(0.f, 0.f);
-    if (ch == 2) return *reinterpret_cast<const float2 *>(in + 2 * f);
-    return make_float2(in[f], 0.f);
+// branch-free: the address is clamped into the buffer, padding frames read as 0
+template <int CH>
+__device__ __forceinline__ float2 load_in(const float *in, int64_t f, int64_t N_in) {
+    const int64_t fc = min(f, N_in - 1);
+    float2 v;
+    if constexpr (CH == 2) v = *reinterpret_cast<const float2 *>(in + 2 * fc);
+    else v = make_float2(in[fc], 0.f);
+    return f < N_in ? v : make_float2(0.f, 0.f);
 }
 
-template <int NS, bool PASS2>
+template <int NS, bool PASS2, int CH>
 __global__ void __launch_bounds__(256) eq_kernel(StageArgs a) {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= a.G) return;
     const int64_t f0 = g * a.T;
     const int len = (int)min((int64_t)a.T, a.N_proc - f0);
-    const int ch = a.ch;
+    constexpr int ch = CH;
     constexpr int D = 8;  // state stride per channel (MM_MAX_DIM), unused entries 0
     double zl[NS][2], zr[NS][2];
     if (PASS2) {
@@ -109,9 +113,9 @@ __global__ void __launch_bounds__(256) eq_kernel(StageArgs a) {
         for (int k = 0; k < NS; ++k) zl[k][0] = zl[k][1] = zr[k][0] = zr[k][1] = 0.0;
     }
     const double(*sos)[5] = a.sos;
-    int ln = 0, pn = 0;
+    int pn = 0;
     stream<8, 3, float2>(
-        len, [&]() { return load_in(a.in, f0 + ln++, a.N_in, ch); },
+        len, [&](int i) { return load_in<CH>(a.in, f0 + min(i, len - 1), a.N_in); },
         [&](float2 v) {
             float l = v.x, r = v.y;
             if (a.sat.on) {
@@ -151,14 +155,15 @@ __global__ void __launch_bounds__(256) eq_kernel(StageArgs a) {
 
 // No active EQ stage: the chain stays f32 (AME:152-162 returns the f32 input;
 // width then runs in f32).
+template <int CH>
 __global__ void __launch_bounds__(256) pre_pointwise_kernel(StageArgs a) {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= a.G) return;
     const int64_t f0 = g * a.T;
     const int len = (int)min((int64_t)a.T, a.N_proc - f0);
-    int ln = 0, pn = 0;
+    int pn = 0;
     stream<8, 2, float2>(
-        len, [&]() { return load_in(a.in, f0 + ln++, a.N_in, a.ch); },
+        len, [&](int i) { return load_in<CH>(a.in, f0 + min(i, len - 1), a.N_in); },
         [&](float2 v) {
             float l = v.x, r = v.y;
             if (a.sat.on) {
@@ -206,9 +211,9 @@ __global__ void __launch_bounds__(256) xover_kernel(StageArgs a) {
             }
         }
     const double(*sos)[5] = a.sos;
-    int ln = 0, pn = 0;
+    int pn = 0;
     stream<8, 3, short2>(
-        len, [&]() { return a.q_in[(int64_t)(ln++) * a.G + g]; },
+        len, [&](int i) { return a.q_in[(int64_t)min(i, len - 1) * a.G + g]; },
         [&](short2 q) {
             const double x[2] = {(double)((float)q.x / 32768.0f), (double)((float)q.y / 32768.0f)};
             int32_t ob0[2] = {0, 0}, ob1[2] = {0, 0}, ob2[2] = {0, 0};
@@ -247,331 +252,6 @@ __global__ void __launch_bounds__(256) xover_kernel(StageArgs a) {
     }
 }
 
-// ------------------------------------------------------ stage C: compressor
-// pydub compress_dynamic_range per band (AME:207-209), restated in SURVEY.md
-// Appendix A.  rms over frames [max(chunk0, i-look), i) (excludes i), both
-// channels: audioop.rms = (unsigned)sqrt(S/n) which, for integer S and
-// n <= 2^12, equals isqrt(S div n) exactly (tests/test_oracle.py).
-// Max attenuation M(rms) comes from a host table built with pydub's own float
-// expressions; inc/dec are M/attack_frames, M/release_frames (correctly
-// rounded).  'above' (rms > thresh) == (M != 0).
-
-__device__ __forceinline__ int32_t frame_energy(short2 v) {
-    return (int32_t)v.x * v.x + (int32_t)v.y * v.y;
-}
-
-// largest r with n*r*r <= S (== trunc(sqrt(S/n)) computed in doubles)
-__device__ __forceinline__ uint32_t rms_exact(int64_t S, int64_t n, float inv_n) {
-    if (n <= 0) return 0;
-    int64_t r = (int64_t)__fsqrt_rn((float)S * inv_n);
-    while (r > 0 && n * r * r > S) --r;
-    while (n * (r + 1) * (r + 1) <= S) ++r;
-    return (uint32_t)r;
-}
-
-// tile-major address of timeline frame f
-__device__ __forceinline__ int64_t tm_index(int64_t f, int T, int64_t G) {
-    int64_t g = f / T;
-    return (f - g * T) * G + g;
-}
-
-// M[b][n*G+g] for every frame.  grid: (ceil(G/256), 3 bands)
-__global__ void __launch_bounds__(256) comp_rms_kernel(CompArgs a) {
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int b = blockIdx.y;
-    if (g >= a.G) return;
-    const short2 *x = a.band[b];
-    const double *lut = a.max_att[b];
-    const int look = a.look[b];
-    const int T = a.T;
-    const int64_t G = a.G;
-    const int64_t f0 = g * T;
-    const int64_t chunk0 = (g / a.K) * a.K * T;
-    const int len = (int)min((int64_t)T, a.N_proc - f0);
-    const int ch = a.ch;
-    // initial window [lo0, f0), lo0 = max(chunk0, f0 - look)
-    const int64_t lo0 = max(chunk0, f0 - look);
-    int64_t S = 0;
-    {
-        int64_t wf = lo0;
-        stream<8, 2, short2>(
-            (int)(f0 - lo0), [&]() { return x[tm_index(wf++, T, G)]; },
-            [&](short2 v) { S += frame_energy(v); });
-    }
-    double *M = a.M[b];
-    int64_t cnt_frames = f0 - lo0;
-    float inv = cnt_frames > 0 ? 1.0f / (float)(cnt_frames * ch) : 0.f;
-    // two streams in lockstep: the new frame f and the dropped frame f - look
-    int64_t lf = f0, pf = f0;
-    struct Pair {
-        short2 in, drop;
-    };
-    stream<8, 3, Pair>(
-        len,
-        [&]() {
-            Pair p;
-            p.in = x[tm_index(lf, T, G)];
-            const int64_t fd = lf - look;
-            p.drop = fd >= chunk0 ? x[tm_index(fd, T, G)] : make_short2(0, 0);
-            ++lf;
-            return p;
-        },
-        [&](Pair p) {
-            const uint32_t r = rms_exact(S, cnt_frames * ch, inv);
-            M[(pf - f0) * G + g] = lut[r];
-            S += frame_energy(p.in);
-            if (pf - look >= chunk0) {
-                S -= frame_energy(p.drop);
-            } else {
-                ++cnt_frames;
-                inv = 1.0f / (float)(cnt_frames * ch);
-            }
-            ++pf;
-        });
-}
-
-// correctly rounded m / d given rd = RN(1/d) (Markstein; tests/test_oracle.py)
-__device__ __forceinline__ double div_cr(double m, double d, double rd) {
-    double q = m * rd;
-    double rem = fma(-q, d, m);
-    return fma(rem, rd, q);
-}
-
-struct BandStep {
-    double A, R, rA, rR;
-};
-
-__device__ __forceinline__ double comp_step(double att, double M, const BandStep &bs) {
-    // both candidates are computed off the att chain's critical path
-    const double inc = div_cr(M, bs.A, bs.rA);
-    const double dec = div_cr(M, bs.R, bs.rR);
-    double up = att + inc;
-    up = (M < up) ? M : up;
-    double dn = att - dec;
-    dn = (0.0 > dn) ? 0.0 : dn;
-    return (M != 0.0 && att <= M) ? up : dn;
-}
-
-__device__ __forceinline__ BandStep band_step(const CompArgs &a, int b) {
-    BandStep s;
-    s.A = a.attack_frames[b];
-    s.R = a.release_frames[b];
-    s.rA = a.rcp_attack[b];
-    s.rR = a.rcp_release[b];
-    return s;
-}
-
-// A super-tile = up to S consecutive tiles of one chunk, the unit of the
-// speculative envelope solve (fewer, longer units -> fewer Jacobi sweeps).
-struct Super {
-    int64_t g0, g1;  // tiles [g0, g1)
-    int len;         // frames
-};
-
-__device__ __forceinline__ Super super_of(const CompArgs &a, int64_t s) {
-    const int64_t KS = (a.K + a.S - 1) / a.S;
-    const int64_t c = s / KS, k = s - c * KS;
-    Super r;
-    r.g0 = c * a.K + k * a.S;
-    r.g1 = min(min(r.g0 + a.S, (c + 1) * a.K), a.G);
-    if (r.g0 >= r.g1) {
-        r.len = 0;
-        r.g1 = r.g0;
-    } else {
-        r.len = (int)(min((int64_t)(r.g1) * a.T, a.N_proc) - r.g0 * a.T);
-    }
-    return r;
-}
-
-// Walk the envelope over a super-tile; optionally record the state at every
-// tile start (tstart) and report whether every frame had M == 0 (identity).
-template <bool RECORD>
-__device__ __forceinline__ double comp_walk(double att, const double *M, const CompArgs &a, const Super &st,
-                                            const BandStep &bs, double *tstart, int &ident) {
-    const int T = a.T;
-    const int64_t G = a.G;
-    int64_t lg = st.g0, pg = st.g0;
-    int ln = 0, pn = 0;
-    int id = 1;
-    stream<8, 4, double>(
-        st.len,
-        [&]() {
-            double v = M[(int64_t)ln * G + lg];
-            if (++ln == T) {
-                ln = 0;
-                ++lg;
-            }
-            return v;
-        },
-        [&](double m) {
-            if (RECORD && pn == 0) tstart[pg] = att;
-            id &= (m == 0.0);
-            att = comp_step(att, m, bs);
-            if (++pn == T) {
-                pn = 0;
-                ++pg;
-            }
-        });
-    ident = id;
-    return att;
-}
-
-// Speculative pass over super-tiles: each starts from a warm-up run over the
-// preceding super-tile of its chunk (from 0); the first super-tile of a chunk
-// starts exactly at 0.  Flags identity super-tiles (att held exactly).
-// grid: (ceil(GS/256), 3)
-__global__ void __launch_bounds__(256) comp_pass0_kernel(CompArgs a) {
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int b = blockIdx.y;
-    if (s >= a.GS) return;
-    const BandStep bs = band_step(a, b);
-    const double *M = a.M[b];
-    const Super st = super_of(a, s);
-    const int64_t KS = (a.K + a.S - 1) / a.S;
-    double att = 0.0;
-    int ident = 1;
-    if (a.warmup > 0 && (s % KS) != 0) {
-        const Super pv = super_of(a, s - 1);
-        att = comp_walk<false>(att, M, a, pv, bs, nullptr, ident);
-    }
-    a.start[b][s] = att;
-    att = comp_walk<true>(att, M, a, st, bs, a.tstart[b], ident);
-    a.end_out[b][s] = att;
-    a.ident[b][s] = st.len == 0 ? 1 : ident;
-}
-
-// prev_active[s] = largest p < s in s's chunk with !ident[p], else -1.
-// One 1024-thread block per (chunk, band): serial runs + Kogge-Stone max-scan.
-__global__ void __launch_bounds__(1024) comp_prev_active_kernel(CompArgs a) {
-    __shared__ int64_t buf[1024];
-    const int b = blockIdx.y;
-    const int64_t KS = (a.K + a.S - 1) / a.S;
-    const int64_t t0 = (int64_t)blockIdx.x * KS;
-    const int64_t n = min(KS, a.GS - t0);
-    const int64_t c = (n + 1023) / 1024;
-    const int tid = threadIdx.x;
-    const int64_t b0 = tid * c, b1 = min(b0 + c, n);
-    int64_t last = -1;
-    for (int64_t m = b0; m < b1; ++m)
-        if (!a.ident[b][t0 + m]) last = t0 + m;
-    buf[tid] = last;
-    __syncthreads();
-    int64_t v = last;
-    for (int d = 1; d < 1024; d <<= 1) {
-        int64_t o = tid >= d ? buf[tid - d] : -1;
-        __syncthreads();
-        v = max(v, o);
-        buf[tid] = v;
-        __syncthreads();
-    }
-    int64_t run = tid > 0 ? buf[tid - 1] : -1;
-    for (int64_t m = b0; m < b1; ++m) {
-        a.prev_active[b][t0 + m] = (int32_t)run;
-        if (!a.ident[b][t0 + m]) run = t0 + m;
-    }
-}
-
-// One Jacobi sweep: an active super-tile whose start differs from the end of
-// its nearest active predecessor (identity super-tiles in between hold att
-// exactly) is re-run from that end.  Exact at convergence (every start == true
-// state, by induction from the exact chunk start).  A sweep that follows a
-// sweep which changed nothing exits at once (converged), so the host queues
-// several per synchronisation.
-__global__ void __launch_bounds__(256) comp_fix_kernel(CompArgs a, const unsigned int *prev_changed) {
-    if (prev_changed && *prev_changed == 0u) return;
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int b = blockIdx.y;
-    if (s >= a.GS) return;
-    const double *end_in = a.end_in[b];
-    double e = end_in[s];
-    if (!a.ident[b][s]) {
-        const int32_t p = a.prev_active[b][s];
-        const double want = p >= 0 ? end_in[p] : 0.0;
-        const double have = a.start[b][s];
-        if (__double_as_longlong(want) != __double_as_longlong(have)) {
-            const BandStep bs = band_step(a, b);
-            const Super st = super_of(a, s);
-            int ident;
-            e = comp_walk<true>(want, a.M[b], a, st, bs, a.tstart[b], ident);
-            a.start[b][s] = want;
-            *a.changed = 1u;  // benign race: every writer stores 1
-        }
-    }
-    a.end_out[b][s] = e;
-}
-
-// Tile starts of identity super-tiles (att held == end of the nearest active
-// predecessor); active super-tiles already recorded theirs.  grid (ceil(G/256), 3)
-__global__ void __launch_bounds__(256) comp_hold_starts_kernel(CompArgs a) {
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int b = blockIdx.y;
-    if (g >= a.G) return;
-    const int64_t KS = (a.K + a.S - 1) / a.S;
-    const int64_t c = g / a.K;
-    const int64_t s = c * KS + (g - c * a.K) / a.S;
-    if (a.ident[b][s]) {
-        const int32_t p = a.prev_active[b][s];
-        a.tstart[b][g] = p >= 0 ? a.end_in[b][p] : 0.0;
-    }
-}
-
-// Final pass per tile: exact trajectory from the converged tile starts; gains
-// applied to the three band samples (audioop.mul floor), overlay
-// sat16(sat16(lo+mid)+hi) (AME:210) -> q2.
-__global__ void __launch_bounds__(256) comp_apply_kernel(CompArgs a) {
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= a.G) return;
-    BandStep bs[3];
-    double att[3];
-#pragma unroll
-    for (int b = 0; b < 3; ++b) {
-        bs[b] = band_step(a, b);
-        att[b] = a.tstart[b][g];
-    }
-    const int64_t G = a.G;
-    const int64_t f0 = g * a.T;
-    const int len = (int)min((int64_t)a.T, a.N_proc - f0);
-    struct Fr {
-        double m[3];
-        short2 v[3];
-    };
-    int ln = 0, pn = 0;
-    stream<4, 2, Fr>(
-        len,
-        [&]() {
-            Fr f;
-            const int64_t idx = (int64_t)(ln++) * G + g;
-#pragma unroll
-            for (int b = 0; b < 3; ++b) {
-                f.m[b] = a.M[b][idx];
-                f.v[b] = a.band[b][idx];
-            }
-            return f;
-        },
-        [&](const Fr &f) {
-            int32_t accl = 0, accr = 0;
-#pragma unroll
-            for (int b = 0; b < 3; ++b) {
-                att[b] = comp_step(att[b], f.m[b], bs[b]);
-                short2 s = f.v[b];
-                if (att[b] != 0.0) {
-                    const double gain = exp10(-att[b] / 20.0);
-                    s.x = audioop_mul(s.x, gain);
-                    s.y = audioop_mul(s.y, gain);
-                }
-                if (b == 0) {
-                    accl = s.x;
-                    accr = s.y;
-                } else {
-                    accl = sat16(accl + s.x);
-                    accr = sat16(accr + s.y);
-                }
-            }
-            a.q_out[(int64_t)(pn++) * G + g] =
-                make_short2((int16_t)accl, a.ch == 2 ? (int16_t)accr : (int16_t)0);
-        });
-}
-
 // ------------------------------------------------- stage D: K-weighting
 // pyloudnorm Meter (AME:213-218): mono = f32 mean(L,R) (= (L+R)/65536 exactly),
 // high_shelf lfilter in f64 stored back to f32, high_pass lfilter in f64
@@ -608,9 +288,8 @@ __global__ void __launch_bounds__(256) kweight_kernel(KwArgs a) {
     }
     double e0 = 0.0, e1 = 0.0;
     int64_t pf = f0;
-    int ln = 0;
     stream<8, 3, short2>(
-        len, [&]() { return a.mix[(int64_t)(ln++) * a.G + g]; },
+        len, [&](int i) { return a.mix[(int64_t)min(i, len - 1) * a.G + g]; },
         [&](short2 q) {
             float m = a.ch == 2 ? ((float)q.x + (float)q.y) * (1.0f / 65536.0f) : (float)q.x * (1.0f / 32768.0f);
             double y1 = df2t((double)m, z[0][0], z[0][1], a.sos[0]);
@@ -743,14 +422,6 @@ __global__ void mix_to_natural_kernel(const short2 *mix, int16_t *out, int64_t G
 }
 
 // explicit instantiations used by the host
-template __global__ void eq_kernel<1, false>(StageArgs);
-template __global__ void eq_kernel<2, false>(StageArgs);
-template __global__ void eq_kernel<3, false>(StageArgs);
-template __global__ void eq_kernel<4, false>(StageArgs);
-template __global__ void eq_kernel<1, true>(StageArgs);
-template __global__ void eq_kernel<2, true>(StageArgs);
-template __global__ void eq_kernel<3, true>(StageArgs);
-template __global__ void eq_kernel<4, true>(StageArgs);
 template __global__ void xover_kernel<false>(StageArgs);
 template __global__ void xover_kernel<true>(StageArgs);
 template __global__ void kweight_kernel<false>(KwArgs);

@@ -13,6 +13,7 @@
 
 #include "../../include/mastering.h"
 #include "kernels.hip"
+#include "compressor.hip"
 #include "scan.hip"
 
 using namespace mm;
@@ -52,6 +53,9 @@ struct mm_ctx {
     std::vector<hipEvent_t> free_events;
     std::map<std::string, KStat> stats;
     std::vector<std::string> stat_order;
+    // host tables already resident on the device
+    const double *lut_src[3] = {nullptr, nullptr, nullptr};
+    std::map<std::string, std::vector<double>> mats_cache;
     // rccl
     ncclComm_t comm = nullptr;
     int rank = 0, nranks = 1;
@@ -148,36 +152,58 @@ static void resolve_events(mm_ctx *c) {
 static inline unsigned blocks_for(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
 
 // ------------------------------------------------------------------ scan
+// Carry-in state of every tile (scan.hip): block-local scan, block-carry scan,
+// apply.  The transition powers are uploaded only when they change.
 static int run_scan(mm_ctx *c, const char *name, const mm_iir &f, int dim, int ch, int64_t line_tiles,
                     int64_t G, const double *z, double *s, const double *init, double *line_end) {
-    const int64_t lines = ((G + line_tiles - 1) / line_tiles) * ch;
-    const int64_t c_needed = (line_tiles + SCAN_THREADS - 1) / SCAN_THREADS;
+    const int64_t nblk = (G + SCAN_BLOCK - 1) / SCAN_BLOCK;
+    const int64_t c_needed = std::max<int64_t>(1, (nblk + SCAN_THREADS - 1) / SCAN_THREADS);
     if (f.scan_c != c_needed)
-        return set_err(c, MM_ERR_ARG, "%s: scan powers built for c=%d, need %lld", name, f.scan_c,
+        return set_err(c, MM_ERR_ARG, "%s: block powers built for c=%d, need %lld", name, f.scan_c,
                        (long long)c_needed);
+    std::vector<double> host((size_t)MAT_COUNT * 64);
+    memcpy(&host[MAT_PHI * 64], f.phi, 64 * sizeof(double));
+    memcpy(&host[MAT_POW2 * 64], f.phi_pow, 12 * 64 * sizeof(double));
+    memcpy(&host[MAT_BLK * 64], f.phi_blk, 64 * sizeof(double));
+    memcpy(&host[MAT_BLKPOW * 64], f.phi_blk_pow, 12 * 64 * sizeof(double));
+    memcpy(&host[MAT_LAST * 64], f.phi_last, 64 * sizeof(double));
+    const std::string key = std::string("mats_") + name;
     double *mats;
-    std::string key = std::string("mats_") + name;
-    RET(get_buf(c, key.c_str(), (size_t)(2 + MM_SCAN_POWERS) * 64, &mats));
-    HIPCHK(c, hipMemcpyAsync(mats, f.phi, 64 * sizeof(double), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(mats + 64, f.phi_pow, MM_SCAN_POWERS * 64 * sizeof(double), hipMemcpyHostToDevice,
-                             c->stream));
-    HIPCHK(c, hipMemcpyAsync(mats + 64 * (1 + MM_SCAN_POWERS), f.phi_last, 64 * sizeof(double),
-                             hipMemcpyHostToDevice, c->stream));
+    RET(get_buf(c, key.c_str(), host.size(), &mats));
+    std::vector<double> &cached = c->mats_cache[key];
+    if (cached != host) {
+        HIPCHK(c, hipMemcpyAsync(mats, host.data(), host.size() * sizeof(double), hipMemcpyHostToDevice,
+                                 c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));  // host vector is transient
+        cached = host;
+    }
     ScanArgs a{};
     a.dim = dim;
-    a.c = (int)c_needed;
     a.ch = ch;
     a.line_tiles = line_tiles;
     a.G = G;
-    a.phi = mats;
-    a.phi_pow = mats + 64;
-    a.phi_last = mats + 64 * (1 + MM_SCAN_POWERS);
+    a.nblk = nblk;
+    a.c = c_needed;
+    a.mats = mats;
     a.z = z;
     a.s = s;
     a.init = init;
     a.line_end = line_end;
-    if (dim == 8) return launch(c, name, scan_kernel<8>, dim3((unsigned)lines), dim3(SCAN_THREADS), 0, a);
-    if (dim == 4) return launch(c, name, scan_kernel<4>, dim3((unsigned)lines), dim3(SCAN_THREADS), 0, a);
+    RET(get_buf(c, (key + "_need").c_str(), (size_t)G * ch, &a.need));
+    RET(get_buf(c, (key + "_agg").c_str(), (size_t)nblk * ch * dim, &a.agg));
+    RET(get_buf(c, (key + "_aggf").c_str(), (size_t)nblk * ch, &a.agg_f));
+    RET(get_buf(c, (key + "_carry").c_str(), (size_t)nblk * ch * dim, &a.carry));
+    const dim3 gl((unsigned)nblk, (unsigned)ch);
+    if (dim == 8) {
+        RET(launch(c, name, scan_local_kernel<8>, gl, dim3(SCAN_BLOCK), 0, a));
+        RET(launch(c, name, scan_blocks_kernel<8>, dim3((unsigned)ch), dim3(SCAN_THREADS), 0, a));
+        return launch(c, name, scan_apply_kernel<8>, gl, dim3(SCAN_BLOCK), 0, a);
+    }
+    if (dim == 4) {
+        RET(launch(c, name, scan_local_kernel<4>, gl, dim3(SCAN_BLOCK), 0, a));
+        RET(launch(c, name, scan_blocks_kernel<4>, dim3((unsigned)ch), dim3(SCAN_THREADS), 0, a));
+        return launch(c, name, scan_apply_kernel<4>, gl, dim3(SCAN_BLOCK), 0, a);
+    }
     return set_err(c, MM_ERR_ARG, "scan dim %d", dim);
 }
 
@@ -211,6 +237,27 @@ static int validate(mm_ctx *c, const mm_job *j) {
 static void fill_sos(double dst[4][5], const mm_iir &f, int n) {
     for (int s = 0; s < 4; ++s)
         for (int k = 0; k < 5; ++k) dst[s][k] = s < n ? f.sos[s][k] : 0.0;
+}
+
+template <int NS, bool P2>
+static int launch_eq_ch(mm_ctx *c, int ch, unsigned nb, const StageArgs &sa) {
+    const char *nm = P2 ? "eq_pass2" : "eq_pass1";
+    if (ch == 2) return launch(c, nm, eq_kernel<NS, P2, 2>, dim3(nb), dim3(256), 0, sa);
+    return launch(c, nm, eq_kernel<NS, P2, 1>, dim3(nb), dim3(256), 0, sa);
+}
+
+template <bool P2>
+static int launch_eq_p(mm_ctx *c, int nsec, int ch, unsigned nb, const StageArgs &sa) {
+    switch (nsec) {
+        case 1: return launch_eq_ch<1, P2>(c, ch, nb, sa);
+        case 2: return launch_eq_ch<2, P2>(c, ch, nb, sa);
+        case 3: return launch_eq_ch<3, P2>(c, ch, nb, sa);
+        default: return launch_eq_ch<4, P2>(c, ch, nb, sa);
+    }
+}
+
+static int launch_eq(mm_ctx *c, int nsec, bool pass2, int ch, unsigned nb, const StageArgs &sa) {
+    return pass2 ? launch_eq_p<true>(c, nsec, ch, nb, sa) : launch_eq_p<false>(c, nsec, ch, nb, sa);
 }
 
 // ------------------------------------------------------------ chain A..C
@@ -249,22 +296,13 @@ static int stage_chunks(mm_ctx *c, const mm_job *j, const float *d_in) {
     if (G > 0) {
         // --- stage A: saturation -> EQ -> width -> int16 (AME:55-63)
         if (j->eq.nsec == 0) {
-            RET(launch(c, "pre_pointwise", pre_pointwise_kernel, dim3(nb), dim3(256), 0, sa));
+            if (ch == 2) RET(launch(c, "pre_pointwise", pre_pointwise_kernel<2>, dim3(nb), dim3(256), 0, sa));
+            else RET(launch(c, "pre_pointwise", pre_pointwise_kernel<1>, dim3(nb), dim3(256), 0, sa));
         } else {
             fill_sos(sa.sos, j->eq, j->eq.nsec);
-            switch (j->eq.nsec) {
-                case 1: RET(launch(c, "eq_pass1", eq_kernel<1, false>, dim3(nb), dim3(256), 0, sa)); break;
-                case 2: RET(launch(c, "eq_pass1", eq_kernel<2, false>, dim3(nb), dim3(256), 0, sa)); break;
-                case 3: RET(launch(c, "eq_pass1", eq_kernel<3, false>, dim3(nb), dim3(256), 0, sa)); break;
-                default: RET(launch(c, "eq_pass1", eq_kernel<4, false>, dim3(nb), dim3(256), 0, sa)); break;
-            }
+            RET(launch_eq(c, j->eq.nsec, false, ch, nb, sa));
             RET(run_scan(c, "eq_scan", j->eq, 8, ch, K, G, z8, s8, nullptr, nullptr));
-            switch (j->eq.nsec) {
-                case 1: RET(launch(c, "eq_pass2", eq_kernel<1, true>, dim3(nb), dim3(256), 0, sa)); break;
-                case 2: RET(launch(c, "eq_pass2", eq_kernel<2, true>, dim3(nb), dim3(256), 0, sa)); break;
-                case 3: RET(launch(c, "eq_pass2", eq_kernel<3, true>, dim3(nb), dim3(256), 0, sa)); break;
-                default: RET(launch(c, "eq_pass2", eq_kernel<4, true>, dim3(nb), dim3(256), 0, sa)); break;
-            }
+            RET(launch_eq(c, j->eq.nsec, true, ch, nb, sa));
         }
     }
     short2 *mix = q1;
@@ -290,10 +328,10 @@ static int stage_chunks(mm_ctx *c, const mm_job *j, const float *d_in) {
         ca.K = K;
         ca.ch = ch;
         ca.warmup = j->comp_warmup;
-        ca.S = std::max(1, j->comp_super);
-        const int64_t KS = (K + ca.S - 1) / ca.S;
+        ca.U = std::max(16, j->comp_super);
         const int64_t nchunks = (G + K - 1) / K;
-        ca.GS = nchunks * KS;
+        ca.SPC = ((int64_t)K * T + ca.U - 1) / ca.U;
+        ca.GS = nchunks * ca.SPC;
         const int64_t GS = ca.GS;
         short2 *q2;
         RET(get_buf(c, "q2", TG, &q2));
@@ -306,34 +344,46 @@ static int stage_chunks(mm_ctx *c, const mm_job *j, const float *d_in) {
         RET(get_buf(c, "comp_lut", (size_t)3 * 32769, &luts));
         unsigned int *changed;
         RET(get_buf(c, "comp_changed", 64, &changed));
-        int32_t *ident, *prev;
-        RET(get_buf(c, "comp_ident", (size_t)3 * GS, &ident));
-        RET(get_buf(c, "comp_prev", (size_t)3 * GS, &prev));
+        int32_t *cnt, *off, *tot;
+        RET(get_buf(c, "comp_cnt", (size_t)3 * G, &cnt));
+        RET(get_buf(c, "comp_off", (size_t)3 * G, &off));
+        RET(get_buf(c, "comp_total", (size_t)3 * nchunks, &tot));
         for (int b = 0; b < 3; ++b) {
-            double *Mb;
+            uint16_t *rb;
+            double *mcb;
             char nm[16];
-            snprintf(nm, sizeof nm, "comp_M%d", b);
-            RET(get_buf(c, nm, TG, &Mb));
-            ca.M[b] = Mb;
+            snprintf(nm, sizeof nm, "comp_r%d", b);
+            RET(get_buf(c, nm, TG, &rb));
+            snprintf(nm, sizeof nm, "comp_Mc%d", b);
+            RET(get_buf(c, nm, (size_t)GS * (ca.U + 1), &mcb));  // + one padding row
+            ca.r16[b] = rb;
+            ca.Mc[b] = mcb;
             ca.band[b] = bands[b];
             ca.max_att[b] = luts + (size_t)b * 32769;
-            HIPCHK(c, hipMemcpyAsync(luts + (size_t)b * 32769, j->band[b].max_att, 32769 * sizeof(double),
-                                     hipMemcpyHostToDevice, c->stream));
+            // tables are immutable host arrays owned by the caller's job: upload once
+            if (c->lut_src[b] != j->band[b].max_att) {
+                HIPCHK(c, hipMemcpyAsync(luts + (size_t)b * 32769, j->band[b].max_att, 32769 * sizeof(double),
+                                         hipMemcpyHostToDevice, c->stream));
+                c->lut_src[b] = j->band[b].max_att;
+            }
+            ca.r0[b] = (uint32_t)j->band[b].r0;
             ca.look[b] = j->band[b].look;
             ca.attack_frames[b] = j->band[b].attack_frames;
             ca.release_frames[b] = j->band[b].release_frames;
             ca.rcp_attack[b] = 1.0 / j->band[b].attack_frames;
             ca.rcp_release[b] = 1.0 / j->band[b].release_frames;
+            ca.cnt[b] = cnt + (size_t)b * G;
+            ca.off[b] = off + (size_t)b * G;
+            ca.total[b] = tot + (size_t)b * nchunks;
             ca.start[b] = st + (size_t)b * GS;
             ca.tstart[b] = tst + (size_t)b * G;
-            ca.ident[b] = ident + (size_t)b * GS;
-            ca.prev_active[b] = prev + (size_t)b * GS;
             ca.end_out[b] = eA + (size_t)b * GS;
         }
         const unsigned nbs = blocks_for(GS, 256);
         RET(launch(c, "comp_rms", comp_rms_kernel, dim3(nb, 3), dim3(256), 0, ca));
+        RET(launch(c, "comp_offsets", comp_offsets_kernel, dim3((unsigned)nchunks, 3), dim3(1024), 0, ca));
+        RET(launch(c, "comp_compact", comp_compact_kernel, dim3(nb, 3), dim3(256), 0, ca));
         RET(launch(c, "comp_pass0", comp_pass0_kernel, dim3(nbs, 3), dim3(256), 0, ca));
-        RET(launch(c, "comp_prev_active", comp_prev_active_kernel, dim3((unsigned)nchunks, 3), dim3(1024), 0, ca));
         // Jacobi sweeps queued in batches: sweep k writes flag k, and exits at once
         // if sweep k-1 changed nothing; one host sync per batch.
         const int batch = 16;
@@ -368,8 +418,8 @@ static int stage_chunks(mm_ctx *c, const mm_job *j, const float *d_in) {
                 return set_err(c, MM_ERR_STATE, "compressor did not converge in %d sweeps", iters);
         }
         c->job.comp_max_iters = iters;  // reported via mm_result
-        for (int b = 0; b < 3; ++b) ca.end_in[b] = cur + (size_t)b * GS;  // converged ends
-        RET(launch(c, "comp_hold_starts", comp_hold_starts_kernel, dim3(nb, 3), dim3(256), 0, ca));
+        RET(launch(c, "comp_record", comp_record_kernel, dim3(nbs, 3), dim3(256), 0, ca));
+        RET(launch(c, "comp_tstart", comp_tstart_kernel, dim3(nb, 3), dim3(256), 0, ca));
         RET(launch(c, "comp_apply", comp_apply_kernel, dim3(nb), dim3(256), 0, ca));
         mix = q2;
     } else {

@@ -191,15 +191,27 @@ def transition_matrix(sections, branches):
     return A
 
 
-def scan_tables(A, tile, line_tiles, last_len):
-    c = max(1, -(-line_tiles // SCAN_THREADS))
+SCAN_BLOCK = 256  # tiles per block of the block-local scan
+
+
+def _doublings(M, n):
+    out = [M]
+    for _ in range(n - 1):
+        out.append(out[-1] @ out[-1])
+    return np.stack(out)
+
+
+def scan_tables(A, tile, total_tiles, last_len):
+    """Transition powers for the three-level tile scan (csrc/scan.hip):
+    phi = A^T, pow2[k] = phi^(2^k), blk = phi^256, blk_pow[k] = blk^(c 2^k) with
+    c = blocks per thread of the block-carry scan, last = A^last_len."""
+    nblk = max(1, -(-total_tiles // SCAN_BLOCK))
+    c = max(1, -(-nblk // SCAN_THREADS))
     phi = np.linalg.matrix_power(A, tile)
-    base = np.linalg.matrix_power(phi, c)
-    pows = [base]
-    for _ in range(SCAN_POWERS - 1):
-        pows.append(pows[-1] @ pows[-1])
-    last = np.linalg.matrix_power(A, last_len)
-    return c, phi, np.stack(pows), last
+    blk = np.linalg.matrix_power(phi, SCAN_BLOCK)
+    return {"c": c, "phi": phi, "pow2": _doublings(phi, SCAN_POWERS), "blk": blk,
+            "blk_pow": _doublings(np.linalg.matrix_power(blk, c), SCAN_POWERS),
+            "last": np.linalg.matrix_power(A, last_len)}
 
 
 # ------------------------------------------------ compressor (pydub constants)

@@ -79,10 +79,10 @@ class Job:
         last_len = self.frames_proc - (G - 1) * self.tile if G else self.tile
         # --- EQ (1 branch)
         eq = design.eq_sections(self.rate, params)
-        self._fill_iir(j.eq, eq, [len(eq)], self.tiles_per_chunk, self.tile)
+        self._fill_iir(j.eq, eq, [len(eq)], max(G, 1), self.tile, last_len)
         # --- crossover (2 branches of 2)
         if multiband:
-            self._fill_iir(j.xover, design.crossover_sections(self.rate), [2, 2], self.tiles_per_chunk, self.tile)
+            self._fill_iir(j.xover, design.crossover_sections(self.rate), [2, 2], max(G, 1), self.tile, last_len)
             self._tables = []
             for b in range(3):
                 tk, td, rk, rd = design.BAND_DEFAULTS[b]
@@ -94,10 +94,12 @@ class Job:
                 jb.thresh_rms, jb.attack_frames, jb.release_frames = bc["thresh_rms"], bc["attack_frames"], \
                     bc["release_frames"]
                 jb.look = bc["look"]
+                nz = np.flatnonzero(tab)
+                jb.r0 = int(nz[0]) if nz.size else 32769
                 jb.max_att = tab.ctypes.data_as(native.c_double_p)
         j.comp_warmup = COMP_WARMUP
         j.comp_max_iters = COMP_MAX_ITERS
-        j.comp_super = max(1, round(COMP_SUPER_FRAMES / self.tile))
+        j.comp_super = COMP_SUPER_FRAMES
         # --- loudness
         if lufs is not None:
             self._fill_iir(j.kweight, design.kweight_sections(self.rate), [2], max(G, 1), self.tile, last_len)
@@ -113,7 +115,7 @@ class Job:
         self.job = j
 
     @staticmethod
-    def _fill_iir(dst, sections, branches, line_tiles, tile, last_len=None):
+    def _fill_iir(dst, sections, branches, total_tiles, tile, last_len=None):
         dst.nsec = len(sections)
         dst.nsec_branch0 = branches[0]
         dst.dim = 2 * len(sections)
@@ -123,11 +125,12 @@ class Job:
         if not sections:
             return
         A = design.transition_matrix(sections, branches)
-        c, phi, pows, last = design.scan_tables(A, tile, line_tiles, last_len or tile)
-        dst.scan_c = c
-        ctypes.memmove(dst.phi, np.ascontiguousarray(phi).ctypes.data, 64 * 8)
-        ctypes.memmove(dst.phi_pow, np.ascontiguousarray(pows).ctypes.data, design.SCAN_POWERS * 64 * 8)
-        ctypes.memmove(dst.phi_last, np.ascontiguousarray(last).ctypes.data, 64 * 8)
+        t = design.scan_tables(A, tile, total_tiles, last_len or tile)
+        dst.scan_c = t["c"]
+        for field, arr in (("phi", t["phi"]), ("phi_pow", t["pow2"]), ("phi_blk", t["blk"]),
+                           ("phi_blk_pow", t["blk_pow"]), ("phi_last", t["last"])):
+            a = np.ascontiguousarray(arr, dtype=np.float64)
+            ctypes.memmove(getattr(dst, field), a.ctypes.data, a.nbytes)
 
 
 def _as_f32_interleaved(pcm: np.ndarray) -> np.ndarray:

@@ -25,12 +25,14 @@ class MMIir(ctypes.Structure):
                 ("scan_c", ctypes.c_int32), ("sos", (ctypes.c_double * 5) * 4),
                 ("phi", ctypes.c_double * (MAX_DIM * MAX_DIM)),
                 ("phi_pow", (ctypes.c_double * (MAX_DIM * MAX_DIM)) * SCAN_POWERS),
+                ("phi_blk", ctypes.c_double * (MAX_DIM * MAX_DIM)),
+                ("phi_blk_pow", (ctypes.c_double * (MAX_DIM * MAX_DIM)) * SCAN_POWERS),
                 ("phi_last", ctypes.c_double * (MAX_DIM * MAX_DIM))]
 
 
 class MMBand(ctypes.Structure):
     _fields_ = [("thresh_rms", ctypes.c_double), ("attack_frames", ctypes.c_double),
-                ("release_frames", ctypes.c_double), ("look", ctypes.c_int32), ("_pad", ctypes.c_int32),
+                ("release_frames", ctypes.c_double), ("look", ctypes.c_int32), ("r0", ctypes.c_int32),
                 ("max_att", c_double_p)]
 
 
