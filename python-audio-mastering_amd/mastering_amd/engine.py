@@ -36,7 +36,12 @@ COMP_SUPER_FRAMES = 1000  # envelope solve unit (frames) -> ~8 Jacobi sweeps on 
 class Job:
     """A planned mastering job: the mm_job POD plus the host arrays it points to."""
 
-    def __init__(self, frames_in: int, rate: int, channels: int, params: dict, out_kind: int = native.MM_OUT_I16):
+    def __init__(self, frames_in: int, rate: int, channels: int, params: dict, out_kind: int = native.MM_OUT_I16,
+                 seg_bounds=None, check_length: bool = True):
+        """`seg_bounds` (time-sharded ranks, distributed.py): this range's loudness
+        segment bounds relative to its first frame; the whole-track gating then
+        happens on the host after the all-reduce.  `check_length=False` skips
+        pyloudnorm's minimum-length check (it applies to the whole track)."""
         if channels not in (1, 2):
             raise ValueError("only mono and stereo are supported (AME:119,137,152)")
         params = dict(params or {})
@@ -58,7 +63,7 @@ class Job:
                 if design.pydub_frame(design.pydub_len_ms(f, self.rate), self.rate) != f:
                     raise NotImplementedError("chunk length not preserved by pydub overlay slicing")
         lufs = params.get("lufs")
-        if lufs is not None and self.frames_proc < 0.4 * self.rate:
+        if check_length and lufs is not None and self.frames_proc < 0.4 * self.rate:
             # pyloudnorm util.valid_audio (AME:218)
             raise ValueError("Audio must have length greater than the block size.")
 
@@ -103,7 +108,11 @@ class Job:
         # --- loudness
         if lufs is not None:
             self._fill_iir(j.kweight, design.kweight_sections(self.rate), [2], max(G, 1), self.tile, last_len)
-            nb, lo, hi, segb, scale = design.loudness_blocks(self.frames_proc, self.rate)
+            if seg_bounds is None:
+                nb, lo, hi, segb, scale = design.loudness_blocks(self.frames_proc, self.rate)
+            else:  # rank-local segments; blocks are gated over the whole track elsewhere
+                segb = np.asarray(seg_bounds, dtype=np.int64)
+                nb, lo, hi, scale = 1, np.zeros(1, np.int64), segb[-1:].copy(), 1.0 / (0.4 * self.rate)
             self._lo, self._hi, self._segb = (np.ascontiguousarray(lo), np.ascontiguousarray(hi),
                                               np.ascontiguousarray(segb))
             j.n_blocks = nb

@@ -1,0 +1,75 @@
+"""The C-ABI boundary on CPU: the HIP library loads, exports every entry point
+include/mastering.h declares, and the ctypes struct layouts in
+mastering_amd/native.py agree with the C compiler's (no compute calls: no GPU)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "mastering.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:int|const char \*)\s*(mm_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_header_declares_the_boundary():
+    fns = declared_functions()
+    for must in ("mm_create", "mm_destroy", "mm_last_error", "mm_master", "mm_master_device", "mm_stage_chunks",
+                 "mm_kweight_range_end", "mm_hop_energies", "mm_finalize", "mm_comm_init",
+                 "mm_allreduce_sum_f64"):
+        assert must in fns
+
+
+def test_library_exports_every_declared_symbol():
+    from mastering_amd import native
+    if not os.path.exists(native.LIB_PATH):
+        pytest.fail(f"HIP library not built: {native.LIB_PATH} (run __graft_entry__.build())")
+    lib = native.load()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    assert sorted(native.EXPORTS) == declared_functions()
+    assert lib.mm_version() >= 1
+
+
+def test_struct_layouts_match_c(tmp_path):
+    from mastering_amd import native
+    prog = tmp_path / "layout.c"
+    fields = {
+        "mm_job": [f[0] for f in native.MMJob._fields_],
+        "mm_iir": [f[0] for f in native.MMIir._fields_],
+        "mm_band": [f[0] for f in native.MMBand._fields_],
+        "mm_result": [f[0] for f in native.MMResult._fields_],
+    }
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "mastering.h"', "int main(void){"]
+    for st, fl in fields.items():
+        lines.append(f'printf("{st} %zu\\n", sizeof({st}));')
+        for f in fl:
+            lines.append(f'printf("{st}.{f} %zu\\n", offsetof({st}, {f}));')
+    lines.append("return 0;}")
+    prog.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)])
+    got = dict(line.rsplit(" ", 1) for line in subprocess.check_output([str(exe)]).decode().splitlines())
+    classes = {"mm_job": native.MMJob, "mm_iir": native.MMIir, "mm_band": native.MMBand,
+               "mm_result": native.MMResult}
+    for st, cls in classes.items():
+        assert int(got[st]) == ctypes.sizeof(cls), st
+        for f in fields[st]:
+            assert int(got[f"{st}.{f}"]) == getattr(cls, f).offset, f"{st}.{f}"
+
+
+def test_product_path_fails_loudly_without_gpu():
+    """No CPU fallback: without a usable device the context cannot be created."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    from mastering_amd import native
+    with pytest.raises(RuntimeError):
+        native.Context(0)

@@ -101,3 +101,69 @@ def test_mix_with_exciter(oracle):
     pcm = pink_noise_pcm16(31 * 44100, 44100, 2, 5)
     mix, ref = _staged_mix(pcm, P_HOT), _oracle_mix(oracle, pcm, P_HOT)
     assert rms_diff(mix, ref) <= RMS_TOL and np.mean(mix == ref) >= 0.999
+
+
+class _ThreadCollectives:
+    """Ranks as threads of one process (one mm_ctx each) on the single GPU."""
+
+    def __init__(self, world):
+        import threading
+        self.world = world
+        self.bar = threading.Barrier(world)
+        self.slots = [None] * world
+
+    def bind(self, rank):
+        outer = self
+
+        class C:
+            def all_gather(self, vec):
+                outer.slots[rank] = np.asarray(vec, np.float64)
+                outer.bar.wait()
+                out = np.stack(outer.slots)
+                outer.bar.wait()
+                return out
+
+            def all_reduce_sum(self, vec):
+                return self.all_gather(vec).sum(axis=0)
+
+        return C()
+
+
+def test_time_sharded_on_one_gpu(oracle):
+    """The C4 orchestration (distributed.master_time_sharded) over the C-ABI with
+    two ranks on one GPU: stitched output == oracle; same loudness on both ranks."""
+    import threading
+
+    import torch
+
+    from mastering_amd import distributed as D
+    from mastering_amd import native
+    from mastering_amd.synth import pink_noise_pcm16
+    rate, world = 44100, 2
+    pcm = pink_noise_pcm16(65 * rate, rate, 2, 9)
+    ref, Lref = oracle.master(pcm, rate, P_FULL, return_loudness=True)
+    coll = _ThreadCollectives(world)
+    outs, infos, errs = [None] * world, [None] * world, []
+
+    def rank_main(r):
+        try:
+            plan = D.plan_time_shards(pcm.shape[0], rate, 2, world, r)
+            be = D.GpuBackend(native.Context(0))
+            x = torch.from_numpy(pcm[plan.in_lo:plan.in_hi].astype(np.float32) / 32768).cuda()
+            out = torch.empty((plan.frames, 2), dtype=torch.int16, device="cuda")
+            infos[r] = D.master_time_sharded(be, plan, P_FULL, x.data_ptr(), out.data_ptr(), coll.bind(r))
+            be.ctx.sync()
+            outs[r] = out.cpu().numpy()
+            be.ctx.close()
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+            coll.bar.abort()
+
+    ts = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=100)
+    assert not errs, errs
+    assert infos[0]["loudness"] == infos[1]["loudness"]
+    _check(np.concatenate(outs), infos[0], ref, Lref)
