@@ -34,7 +34,8 @@ extern "C" {
 #define MM_ERR_STATE (-4)
 
 #define MM_MAX_DIM 8      /* max IIR state dimension per channel (4 biquads) */
-#define MM_SCAN_POWERS 12 /* powers Phi^(c*2^k), k < MM_SCAN_POWERS */
+#define MM_TILE_POW 8     /* Phi_T^(2^k), k < MM_TILE_POW (tiles per block <= 256) */
+#define MM_BLK_POW 65     /* Phi_B^e, e = 0..64 (one look-back window of 64 blocks) */
 
 #define MM_OUT_I16 0 /* interleaved int16 PCM (what AME:89/98 writes)            */
 #define MM_OUT_F32 1 /* interleaved f32 = the same PCM / 32768 (decoded form)    */
@@ -43,24 +44,20 @@ typedef struct mm_ctx mm_ctx;
 
 /* One IIR stage = 1..2 branches of cascaded DF2T biquads fed by the same input.
  * sos[s] = {b0, b1, b2, a1, a2} (a0 == 1), branches laid out branch-major.
- * State-transition matrices (row-major MM_MAX_DIM x MM_MAX_DIM, only dim x dim
- * used) of the zero-input recurrence, for the three-level tile scan:
- *   phi          one tile (A^T)
- *   phi_pow[k]   2^k tiles                          (block-local scan, k < 8)
- *   phi_blk      one block of 256 tiles
- *   phi_blk_pow[k]  256*c*2^k tiles, c = blocks per thread of the block scan
- *   phi_last     the last (possibly partial) tile of the track */
+ * State-transition matrices of the zero-input recurrence (row-major
+ * MM_MAX_DIM x MM_MAX_DIM, only dim x dim used) for the in-kernel tile carry
+ * (csrc/lookback.h):
+ *   phi_tile_pow[k]  Phi_T^(2^k), Phi_T = A^tile (A: one frame)
+ *   phi_blk_pow[e]   Phi_B^e, Phi_B = Phi_T^tpb (tpb = tiles per thread block:
+ *                    128 for stereo stages, 256 for mono ones) */
 typedef struct mm_iir {
     int32_t nsec;            /* total sections (0 = stage inactive)           */
     int32_t nsec_branch0;    /* sections in branch 0 (rest are branch 1)      */
     int32_t dim;             /* state dim per channel = 2 * nsec              */
-    int32_t scan_c;          /* blocks per thread the block powers were made for */
+    int32_t tpb;             /* tiles per block the block powers were made for */
     double sos[4][5];
-    double phi[MM_MAX_DIM * MM_MAX_DIM];
-    double phi_pow[MM_SCAN_POWERS][MM_MAX_DIM * MM_MAX_DIM];
-    double phi_blk[MM_MAX_DIM * MM_MAX_DIM];
-    double phi_blk_pow[MM_SCAN_POWERS][MM_MAX_DIM * MM_MAX_DIM];
-    double phi_last[MM_MAX_DIM * MM_MAX_DIM];
+    double phi_tile_pow[MM_TILE_POW][MM_MAX_DIM * MM_MAX_DIM];
+    double phi_blk_pow[MM_BLK_POW][MM_MAX_DIM * MM_MAX_DIM];
 } mm_iir;
 
 /* Per-band pydub compress_dynamic_range parameters (AME:207-209). */

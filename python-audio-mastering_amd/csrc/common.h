@@ -109,25 +109,6 @@ struct SatArgs {
     int on;
 };
 
-// Arguments of the pre-chain (EQ) and crossover kernels.
-struct StageArgs {
-    const float *in;   // natural interleaved f32 input (stage A)
-    int64_t N_in;      // valid input frames
-    int64_t N_proc;    // processed timeline frames
-    int64_t G;         // tiles
-    int T;             // frames per tile
-    int ch;            // channels (1|2)
-    SatArgs sat;
-    double width;
-    int width_on;
-    double sos[4][5];  // {b0,b1,b2,a1,a2}
-    double *z_out;     // pass 1: per-tile zero-state end state [G][ch][D]
-    const double *s_in;  // pass 2: per-tile carry-in state [G][ch][D]
-    const short2 *q_in;  // tile-major int16 pairs
-    short2 *q_out;
-    short2 *band_out[3];
-};
-
 struct CompArgs {
     int64_t N_proc, G;
     int T, K, ch, warmup;
@@ -153,44 +134,12 @@ struct CompArgs {
     short2 *q_out;
 };
 
-struct KwArgs {
-    int64_t N_proc, G;
-    int T, ch;
-    double sos[2][5];
-    const short2 *mix;
-    double *z_out;
-    const double *s_in;
-    int64_t n_segs;
-    const int64_t *seg_bounds;
-    double *part;      // [G][2]
-    int64_t *part_seg; // [G]
-};
-
 struct FinArgs {
     int64_t N_proc, G;
     int T, ch, out_kind, use_gain;
     double gain;
     const short2 *mix;
     void *out;
-};
-
-// Segmented affine state scan over the tiles of a track (scan.hip).
-struct ScanArgs {
-    int dim;            // state stride per channel (4 or 8)
-    int ch;             // channels interleaved in z/s: [tile][ch][dim]
-    int64_t line_tiles; // state resets to 0 at tiles g % line_tiles == 0
-    int64_t G;          // tiles
-    int64_t nblk;       // blocks of 256 tiles
-    int64_t c;          // blocks per thread in the block scan
-    const double *mats; // device: phi, pow2[12], blk, blk_pow[12], last (8x8 each)
-    const double *z;    // per-tile zero-state end state
-    double *s;          // per-tile carry-in state (output)
-    uint8_t *need;      // [G][ch] tile needs the block carry
-    double *agg;        // [nblk][ch][dim] block aggregates
-    int *agg_f;         // [nblk][ch] reset inside block
-    double *carry;      // [nblk][ch][dim] state at each block start
-    const double *init; // optional state at the track start [ch][dim] (or null)
-    double *line_end;   // optional state after the last tile [ch][dim] (or null)
 };
 
 }  // namespace mm

@@ -1,0 +1,386 @@
+// iir.hip — the three linear-recurrence stages of the chain, one launch each.
+//
+// A lane owns one tile (T frames) of ONE channel: stereo tiles use lane pairs
+// (even lane = left, odd lane = right), which doubles the lanes in flight over a
+// lane-per-tile layout and keeps the per-frame f64 chain short.  Each kernel
+// runs its recurrence twice over the tile: pass 1 from the zero state (end state
+// z), lookback.h's in-kernel carry, pass 2 from the exact carry producing the
+// stage outputs.  Intermediates are tile-major int16 pairs: element (tile g,
+// frame n, channel c) at (n*G + g)*2 + c, so a wave's 64 lanes touch 128
+// consecutive bytes at every step.
+//
+//   eq_kernel      AME:55-63   f32 input -> exciter (f32) -> EQ (<=4 DF2T, f64)
+//                              -> width (f64, lane-pair exchange) -> int16 q1
+//   xover_kernel   AME:196-206 q1/32768 -> LP4 250 Hz + HP4 4 kHz (f64),
+//                              mid = x - lo - hi -> three int16 band planes
+//   kweight_kernel AME:213-218 mix -> mono f32 -> pyloudnorm high shelf + high
+//                              pass (f64, f32 between) -> per-tile energies of
+//                              the 0.1 s loudness segments
+#include "lookback.h"
+
+namespace mm {
+
+// float_array_to_audio_segment (AME:123-126): clip to [-1,1] (NaN propagates),
+// * 32768, astype(int16) == trunc to int32 then wrap to 16 bits; NaN -> 0.
+__device__ __forceinline__ int16_t quantize(double v) {
+    if (v != v) return 0;
+    v = v > 1.0 ? 1.0 : v;
+    v = v < -1.0 ? -1.0 : v;
+    int32_t i = (int32_t)(v * 32768.0);
+    return (int16_t)i;
+}
+
+// apply_saturation (AME:128-134), f32 throughout; no FMA contraction so the
+// rounding sequence matches numpy: keep*x + mix*tanh(x*drive).
+__device__ __forceinline__ float saturate(float x, const SatArgs &s) {
+    float t = tanhf(__fmul_rn(x, s.drive));
+    return __fadd_rn(__fmul_rn(s.keep, x), __fmul_rn(s.mix, t));
+}
+
+// DF2T section (scipy sosfilt / lfilter form): y = b0 x + z0;
+// z0 = b1 x - a1 y + z1; z1 = b2 x - a2 y.  State s = (z0, z1).
+__device__ __forceinline__ double df2t(double x, double &z0, double &z1, const double *c) {
+    double y = fma(c[0], x, z0);
+    double t0 = fma(c[1], x, z1);
+    double t1 = c[2] * x;
+    z0 = fma(-c[3], y, t0);
+    z1 = fma(-c[4], y, t1);
+    return y;
+}
+
+// ------------------------------------------------------------------ EQ stage
+constexpr int EQ_STAGE = 16;  // frames per tile staged through LDS per step
+
+struct EqArgs {
+    const float *in;   // natural interleaved f32 input
+    int64_t N_in;      // valid input frames (later frames read as 0: pydub pads)
+    int64_t N_proc;    // processed frames
+    int64_t G;         // tiles
+    int T;             // frames per tile
+    SatArgs sat;
+    double width;
+    int width_on;
+    double sos[4][5];  // {b0,b1,b2,a1,a2}
+    int16_t *q_out;    // tile-major int16 pairs
+};
+
+template <int CH>
+constexpr int eq_stage_bytes() {
+    return 2 * (LB_THREADS / CH) * (EQ_STAGE + 1) * CH * (int)sizeof(float);
+}
+
+// One pass over the block's tiles with the input staged through LDS: the block
+// cooperatively loads EQ_STAGE frames of each of its tiles (16 consecutive
+// threads read one tile's 128 contiguous bytes), double-buffered so the next
+// stage's loads are in flight while lanes run the recurrence.
+template <int NS, int CH, bool P2>
+__device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, double (&z)[NS][2], float *stage) {
+    constexpr int TPB = LB_THREADS / CH;
+    constexpr int ROW = (EQ_STAGE + 1) * CH;       // floats per staged tile row (padded)
+    constexpr int ITEMS = TPB * EQ_STAGE / LB_THREADS;  // frames each thread loads per step
+    const int T = a.T;
+    const int nsteps = (T + EQ_STAGE - 1) / EQ_STAGE;
+    const int tid = threadIdx.x;
+    const double(*sos)[5] = a.sos;
+    float regs[ITEMS][CH];
+    auto load = [&](int step) {
+#pragma unroll
+        for (int r = 0; r < ITEMS; ++r) {
+            const int idx = tid + r * LB_THREADS;
+            const int tt = idx / EQ_STAGE, j = idx % EQ_STAGE;
+            const int n = step * EQ_STAGE + j;
+            const int64_t f = (g0 + tt) * T + n;
+            const bool ok = n < T && f < a.N_in;  // also excludes tiles past the track end
+            const int64_t fc = ok ? f : 0;
+            if constexpr (CH == 2) {
+                const float2 v = *reinterpret_cast<const float2 *>(a.in + 2 * fc);
+                regs[r][0] = ok ? v.x : 0.f;
+                regs[r][1] = ok ? v.y : 0.f;
+            } else {
+                const float v = a.in[fc];
+                regs[r][0] = ok ? v : 0.f;
+            }
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int r = 0; r < ITEMS; ++r) {
+            const int idx = tid + r * LB_THREADS;
+            const int tt = idx / EQ_STAGE, j = idx % EQ_STAGE;
+            float *dst = stage + buf * TPB * ROW + tt * ROW + j * CH;
+#pragma unroll
+            for (int q = 0; q < CH; ++q) dst[q] = regs[r][q];
+        }
+    };
+    load(0);
+    store(0);
+    __syncthreads();
+    const int64_t g = g0 + t;
+    for (int step = 0; step < nsteps; ++step) {
+        const int cur = step & 1;
+        if (step + 1 < nsteps) load(step + 1);
+        const float *row = stage + cur * TPB * ROW + t * ROW;
+#pragma unroll 4
+        for (int j = 0; j < EQ_STAGE; ++j) {
+            const int n = step * EQ_STAGE + j;
+            if (n >= len) break;
+            float x = row[j * CH + c];
+            if (a.sat.on) x = saturate(x, a.sat);
+            double y = (double)x;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) y = df2t(y, z[s][0], z[s][1], sos[s]);
+            if (P2) {
+                if (CH == 2 && a.width_on) {  // apply_stereo_width (AME:136-144), f64
+                    const double o = __shfl_xor(y, 1);
+                    const double yl = c == 0 ? y : o, yr = c == 0 ? o : y;
+                    const double mid = (yl + yr) / 2;
+                    const double side = (yl - yr) / 2 * a.width;
+                    y = c == 0 ? mid + side : mid - side;
+                }
+                const int64_t o = ((int64_t)n * a.G + g) * 2;
+                if (CH == 2) a.q_out[o + c] = quantize(y);
+                else *reinterpret_cast<short2 *>(a.q_out + o) = make_short2(quantize(y), 0);  // mono: R = 0
+            }
+        }
+        if (step + 1 < nsteps) store(cur ^ 1);
+        __syncthreads();
+    }
+}
+
+template <int NS, int CH>
+__global__ void __launch_bounds__(LB_THREADS, 4) eq_kernel(EqArgs a, LbArgs lb, int64_t line_tiles) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    constexpr int TPB = LB_THREADS / CH;
+    constexpr int DIM = 2 * NS;
+    __shared__ int ticket_slot;
+    const int blk = lb_ticket(lb, &ticket_slot);
+    const int tid = threadIdx.x;
+    const int c = CH == 2 ? (tid & 1) : 0;
+    const int t = tid / CH;
+    const int64_t g0 = (int64_t)blk * TPB;
+    const int64_t g = g0 + t;
+    const bool valid = g < a.G;
+    const int len = valid ? (int)min((int64_t)a.T, a.N_proc - g * a.T) : 0;
+    float *stage = reinterpret_cast<float *>(smem);
+    double *lds = smem + eq_stage_bytes<CH>() / 8;
+    double zs[NS][2];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) zs[s][0] = zs[s][1] = 0.0;
+    eq_pass<NS, CH, false>(a, g0, t, c, len, zs, stage);
+    double z[DIM], s[DIM], rst[DIM];
+#pragma unroll
+    for (int s_ = 0; s_ < NS; ++s_) {
+        z[2 * s_] = zs[s_][0];
+        z[2 * s_ + 1] = zs[s_][1];
+    }
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) rst[d] = 0.0;
+    lb_carry<DIM, CH>(lb, blk, t, c, valid, valid && (g % line_tiles) == 0, rst, z, s, lds);
+#pragma unroll
+    for (int s_ = 0; s_ < NS; ++s_) {
+        zs[s_][0] = s[2 * s_];
+        zs[s_][1] = s[2 * s_ + 1];
+    }
+    eq_pass<NS, CH, true>(a, g0, t, c, len, zs, stage);
+}
+
+// No active EQ stage: the chain stays f32 (AME:152-162 returns the f32 input;
+// width then runs in f32).  Pointwise; natural layout in, tile-major out.
+template <int CH>
+__global__ void __launch_bounds__(256) pre_pointwise_kernel(EqArgs a) {
+    const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= a.N_proc) return;
+    float v[2] = {0.f, 0.f};
+    if (f < a.N_in) {
+        if constexpr (CH == 2) {
+            const float2 x = *reinterpret_cast<const float2 *>(a.in + 2 * f);
+            v[0] = x.x;
+            v[1] = x.y;
+        } else {
+            v[0] = a.in[f];
+        }
+    }
+    if (a.sat.on) {
+        v[0] = saturate(v[0], a.sat);
+        v[1] = saturate(v[1], a.sat);
+    }
+    if (CH == 2 && a.width_on) {
+        const float w = (float)a.width;
+        const float mid = __fdiv_rn(__fadd_rn(v[0], v[1]), 2.0f);
+        const float side = __fmul_rn(__fdiv_rn(__fsub_rn(v[0], v[1]), 2.0f), w);
+        v[0] = __fadd_rn(mid, side);
+        v[1] = __fsub_rn(mid, side);
+    }
+    const int64_t g = f / a.T, n = f - g * a.T;
+    const int64_t o = (n * a.G + g) * 2;
+    a.q_out[o] = quantize((double)v[0]);
+    a.q_out[o + 1] = CH == 2 ? quantize((double)v[1]) : (int16_t)0;
+}
+
+// ------------------------------------------------------------ crossover stage
+struct XoArgs {
+    int64_t N_proc, G;
+    int T;
+    double sos[4][5];     // LP s0, LP s1, HP s0, HP s1
+    const int16_t *q_in;  // tile-major int16 pairs
+    int16_t *band[3];     // low / mid / high planes, same layout
+};
+
+template <int CH, bool P2>
+__device__ __forceinline__ void xo_pass(const XoArgs &a, int64_t g, int c, int len, double (&z)[4][2]) {
+    const double(*sos)[5] = a.sos;
+    const int64_t G = a.G;
+    int pn = 0;
+    stream<8, 3, int16_t>(
+        len, [&](int i) { return a.q_in[((int64_t)min(i, len - 1) * G + g) * 2 + c]; },
+        [&](int16_t q) {
+            const double x = (double)((float)q / 32768.0f);  // AME:199 int16 -> f32
+            double yl = df2t(x, z[0][0], z[0][1], sos[0]);
+            yl = df2t(yl, z[1][0], z[1][1], sos[1]);
+            double yh = df2t(x, z[2][0], z[2][1], sos[2]);
+            yh = df2t(yh, z[3][0], z[3][1], sos[3]);
+            if (P2) {
+                const double ym = (x - yl) - yh;  // AME:202
+                const int64_t o = ((int64_t)pn * G + g) * 2;
+                if (CH == 2) {
+                    a.band[0][o + c] = quantize(yl);
+                    a.band[1][o + c] = quantize(ym);
+                    a.band[2][o + c] = quantize(yh);
+                } else {  // mono: the second half of every pair stays 0
+                    *reinterpret_cast<short2 *>(a.band[0] + o) = make_short2(quantize(yl), 0);
+                    *reinterpret_cast<short2 *>(a.band[1] + o) = make_short2(quantize(ym), 0);
+                    *reinterpret_cast<short2 *>(a.band[2] + o) = make_short2(quantize(yh), 0);
+                }
+            }
+            ++pn;
+        });
+}
+
+template <int CH>
+__global__ void __launch_bounds__(LB_THREADS, 4) xover_kernel(XoArgs a, LbArgs lb, int64_t line_tiles) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    constexpr int TPB = LB_THREADS / CH;
+    __shared__ int ticket_slot;
+    const int blk = lb_ticket(lb, &ticket_slot);
+    const int tid = threadIdx.x;
+    const int c = CH == 2 ? (tid & 1) : 0;
+    const int t = tid / CH;
+    const int64_t g = (int64_t)blk * TPB + t;
+    const bool valid = g < a.G;
+    const int len = valid ? (int)min((int64_t)a.T, a.N_proc - g * a.T) : 0;
+    double zs[4][2] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
+    if (valid) xo_pass<CH, false>(a, g, c, len, zs);
+    double z[8], s[8], rst[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        z[2 * k] = zs[k][0];
+        z[2 * k + 1] = zs[k][1];
+        rst[2 * k] = rst[2 * k + 1] = 0.0;
+    }
+    lb_carry<8, CH>(lb, blk, t, c, valid, valid && (g % line_tiles) == 0, rst, z, s, smem);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        zs[k][0] = s[2 * k];
+        zs[k][1] = s[2 * k + 1];
+    }
+    if (valid) xo_pass<CH, true>(a, g, c, len, zs);
+}
+
+// ----------------------------------------------------------- K-weighting stage
+struct KwArgs {
+    int64_t N_proc, G;
+    int T, ch;
+    double sos[2][5];
+    const int16_t *mix;     // tile-major int16 pairs (pre-gain chain output)
+    int64_t n_segs;
+    const int64_t *seg_bounds;
+    double *part;           // [G][2] energies of the (at most two) segments a tile touches
+    int64_t *part_seg;      // [G]   first segment of the tile
+    double *line_end;       // optional [4]: state after the last frame
+};
+
+// pyloudnorm Meter (AME:213-218): mono = f32 mean(L,R) (== (L+R)/65536 exactly),
+// high_shelf lfilter in f64 stored back to f32, high_pass lfilter in f64 stored
+// to f32, then squared sums per 0.4 s / 0.1 s block.  The whole track is one line.
+template <bool P2>
+__device__ __forceinline__ void kw_pass(const KwArgs &a, int64_t g, int len, double (&z)[2][2], int64_t seg_end,
+                                        double &e0, double &e1) {
+    const int64_t G = a.G;
+    const short2 *mix = reinterpret_cast<const short2 *>(a.mix);
+    int64_t pf = g * a.T;
+    stream<8, 3, short2>(
+        len, [&](int i) { return mix[(int64_t)min(i, len - 1) * G + g]; },
+        [&](short2 q) {
+            const float m = a.ch == 2 ? ((float)q.x + (float)q.y) * (1.0f / 65536.0f)
+                                      : (float)q.x * (1.0f / 32768.0f);
+            const double y1 = df2t((double)m, z[0][0], z[0][1], a.sos[0]);
+            const float y1f = (float)y1;
+            const double y2 = df2t((double)y1f, z[1][0], z[1][1], a.sos[1]);
+            if (P2) {
+                const float y2f = (float)y2;
+                const double e = (double)y2f * (double)y2f;
+                if (pf < seg_end) e0 += e;
+                else e1 += e;
+            }
+            ++pf;
+        });
+}
+
+__global__ void __launch_bounds__(LB_THREADS, 2) kweight_kernel(KwArgs a, LbArgs lb) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    __shared__ int ticket_slot;
+    const int blk = lb_ticket(lb, &ticket_slot);
+    const int t = threadIdx.x;
+    const int64_t g = (int64_t)blk * LB_THREADS + t;
+    const bool valid = g < a.G;
+    const int len = valid ? (int)min((int64_t)a.T, a.N_proc - g * a.T) : 0;
+    double zs[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
+    double e0 = 0.0, e1 = 0.0;
+    if (valid) kw_pass<false>(a, g, len, zs, 0, e0, e1);
+    double z[4] = {zs[0][0], zs[0][1], zs[1][0], zs[1][1]}, s[4], rst[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) rst[d] = lb.init ? lb.init[d] : 0.0;
+    lb_carry<4, 1>(lb, blk, t, 0, valid, valid && g == 0, rst, z, s, smem);
+    if (!valid) return;
+    // loudness segment of the tile's first frame (largest s with bounds[s] <= f0)
+    const int64_t f0 = g * a.T;
+    int64_t lo = 0, hi = a.n_segs;
+    while (hi - lo > 1) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (a.seg_bounds[mid] <= f0) lo = mid;
+        else hi = mid;
+    }
+    zs[0][0] = s[0];
+    zs[0][1] = s[1];
+    zs[1][0] = s[2];
+    zs[1][1] = s[3];
+    kw_pass<true>(a, g, len, zs, a.seg_bounds[lo + 1], e0, e1);
+    a.part[2 * g] = e0;
+    a.part[2 * g + 1] = e1;
+    a.part_seg[g] = lo;
+    if (a.line_end && g == a.G - 1) {
+        a.line_end[0] = zs[0][0];
+        a.line_end[1] = zs[0][1];
+        a.line_end[2] = zs[1][0];
+        a.line_end[3] = zs[1][1];
+    }
+}
+
+// Sum the per-tile partials into loudness segments (deterministic order).
+__global__ void seg_reduce_kernel(KwArgs a, double *seg_energy) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= a.n_segs) return;
+    int64_t b0 = a.seg_bounds[s], b1 = a.seg_bounds[s + 1];
+    if (b1 > a.N_proc) b1 = a.N_proc;
+    double acc = 0.0;
+    if (b0 < b1) {
+        const int64_t g0 = b0 / a.T, g1 = (b1 - 1) / a.T;
+        for (int64_t g = g0; g <= g1; ++g) {
+            if (a.part_seg[g] == s) acc += a.part[2 * g];
+            else if (a.part_seg[g] == s - 1) acc += a.part[2 * g + 1];
+        }
+    }
+    seg_energy[s] = acc;
+}
+
+}  // namespace mm

@@ -12,9 +12,9 @@
 #include <vector>
 
 #include "../../include/mastering.h"
+#include "iir.hip"
 #include "kernels.hip"
 #include "compressor.hip"
-#include "scan.hip"
 
 using namespace mm;
 
@@ -47,6 +47,7 @@ struct mm_ctx {
     mm_job job{};
     int64_t G = 0;
     short2 *mix = nullptr;
+    unsigned *lb_error = nullptr;
     // timing
     bool timing = false;
     std::vector<PendingEvent> pending;
@@ -151,60 +152,41 @@ static void resolve_events(mm_ctx *c) {
 
 static inline unsigned blocks_for(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
 
-// ------------------------------------------------------------------ scan
-// Carry-in state of every tile (scan.hip): block-local scan, block-carry scan,
-// apply.  The transition powers are uploaded only when they change.
-static int run_scan(mm_ctx *c, const char *name, const mm_iir &f, int dim, int ch, int64_t line_tiles,
-                    int64_t G, const double *z, double *s, const double *init, double *line_end) {
-    const int64_t nblk = (G + SCAN_BLOCK - 1) / SCAN_BLOCK;
-    const int64_t c_needed = std::max<int64_t>(1, (nblk + SCAN_THREADS - 1) / SCAN_THREADS);
-    if (f.scan_c != c_needed)
-        return set_err(c, MM_ERR_ARG, "%s: block powers built for c=%d, need %lld", name, f.scan_c,
-                       (long long)c_needed);
-    std::vector<double> host((size_t)MAT_COUNT * 64);
-    memcpy(&host[MAT_PHI * 64], f.phi, 64 * sizeof(double));
-    memcpy(&host[MAT_POW2 * 64], f.phi_pow, 12 * 64 * sizeof(double));
-    memcpy(&host[MAT_BLK * 64], f.phi_blk, 64 * sizeof(double));
-    memcpy(&host[MAT_BLKPOW * 64], f.phi_blk_pow, 12 * 64 * sizeof(double));
-    memcpy(&host[MAT_LAST * 64], f.phi_last, 64 * sizeof(double));
-    const std::string key = std::string("mats_") + name;
-    double *mats;
-    RET(get_buf(c, key.c_str(), host.size(), &mats));
+// ------------------------------------------------------- look-back plumbing
+// Transition tables of one filter stage (uploaded only when they change).
+static int upload_tables(mm_ctx *c, const char *name, const mm_iir &f, LbArgs &lb) {
+    const size_t n = (size_t)(MM_TILE_POW + MM_BLK_POW) * 64;
+    std::vector<double> host(n);
+    memcpy(host.data(), f.phi_tile_pow, sizeof f.phi_tile_pow);
+    memcpy(host.data() + MM_TILE_POW * 64, f.phi_blk_pow, sizeof f.phi_blk_pow);
+    const std::string key = std::string("tab_") + name;
+    double *d;
+    RET(get_buf(c, key.c_str(), n, &d));
     std::vector<double> &cached = c->mats_cache[key];
     if (cached != host) {
-        HIPCHK(c, hipMemcpyAsync(mats, host.data(), host.size() * sizeof(double), hipMemcpyHostToDevice,
-                                 c->stream));
+        HIPCHK(c, hipMemcpyAsync(d, host.data(), n * sizeof(double), hipMemcpyHostToDevice, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));  // host vector is transient
         cached = host;
     }
-    ScanArgs a{};
-    a.dim = dim;
-    a.ch = ch;
-    a.line_tiles = line_tiles;
-    a.G = G;
-    a.nblk = nblk;
-    a.c = c_needed;
-    a.mats = mats;
-    a.z = z;
-    a.s = s;
-    a.init = init;
-    a.line_end = line_end;
-    RET(get_buf(c, (key + "_need").c_str(), (size_t)G * ch, &a.need));
-    RET(get_buf(c, (key + "_agg").c_str(), (size_t)nblk * ch * dim, &a.agg));
-    RET(get_buf(c, (key + "_aggf").c_str(), (size_t)nblk * ch, &a.agg_f));
-    RET(get_buf(c, (key + "_carry").c_str(), (size_t)nblk * ch * dim, &a.carry));
-    const dim3 gl((unsigned)nblk, (unsigned)ch);
-    if (dim == 8) {
-        RET(launch(c, name, scan_local_kernel<8>, gl, dim3(SCAN_BLOCK), 0, a));
-        RET(launch(c, name, scan_blocks_kernel<8>, dim3((unsigned)ch), dim3(SCAN_THREADS), 0, a));
-        return launch(c, name, scan_apply_kernel<8>, gl, dim3(SCAN_BLOCK), 0, a);
-    }
-    if (dim == 4) {
-        RET(launch(c, name, scan_local_kernel<4>, gl, dim3(SCAN_BLOCK), 0, a));
-        RET(launch(c, name, scan_blocks_kernel<4>, dim3((unsigned)ch), dim3(SCAN_THREADS), 0, a));
-        return launch(c, name, scan_apply_kernel<4>, gl, dim3(SCAN_BLOCK), 0, a);
-    }
-    return set_err(c, MM_ERR_ARG, "scan dim %d", dim);
+    lb.pw_tile = d;
+    lb.pw_blk = d + MM_TILE_POW * 64;
+    return MM_OK;
+}
+
+// Per-launch look-back state for nblk blocks of CH lines: the ticket and the
+// status words are zeroed by a memset on the stream right before the launch.
+static int lb_prepare(mm_ctx *c, int64_t nblk, int ch, LbArgs &lb) {
+    const size_t flag_bytes = ((16 + (size_t)nblk * 4) + 15) / 16 * 16;
+    char *flags;
+    RET(get_buf(c, "lb_flags", flag_bytes, &flags));
+    HIPCHK(c, hipMemsetAsync(flags, 0, flag_bytes, c->stream));
+    lb.ticket = reinterpret_cast<unsigned *>(flags);
+    lb.status = reinterpret_cast<unsigned *>(flags + 16);
+    RET(get_buf(c, "lb_agg", (size_t)nblk * ch * 8, &lb.agg));
+    RET(get_buf(c, "lb_incl", (size_t)nblk * ch * 8, &lb.incl));
+    RET(get_buf(c, "lb_error", 4, &lb.error));
+    lb.init = nullptr;
+    return MM_OK;
 }
 
 static int validate(mm_ctx *c, const mm_job *j) {
@@ -214,6 +196,10 @@ static int validate(mm_ctx *c, const mm_job *j) {
     if (j->tiles_per_chunk < 1) return set_err(c, MM_ERR_ARG, "tiles_per_chunk < 1");
     if (j->frames_proc < 0 || j->frames_in < 0) return set_err(c, MM_ERR_ARG, "negative frame count");
     if (j->eq.nsec < 0 || j->eq.nsec > 4) return set_err(c, MM_ERR_ARG, "eq.nsec %d", j->eq.nsec);
+    const int tpb = LB_THREADS / j->channels;
+    if (j->eq.nsec > 0 && j->eq.tpb != tpb) return set_err(c, MM_ERR_ARG, "eq tables built for %d tiles/block, need %d", j->eq.tpb, tpb);
+    if (j->multiband_on && j->xover.tpb != tpb) return set_err(c, MM_ERR_ARG, "crossover tables built for %d tiles/block", j->xover.tpb);
+    if (j->lufs_on && j->kweight.tpb != LB_THREADS) return set_err(c, MM_ERR_ARG, "K-weighting tables built for %d tiles/block", j->kweight.tpb);
     if (j->multiband_on) {
         if (j->xover.nsec != 4 || j->xover.nsec_branch0 != 2) return set_err(c, MM_ERR_ARG, "crossover must be 2+2 sections");
         for (int b = 0; b < 3; ++b) {
@@ -239,25 +225,23 @@ static void fill_sos(double dst[4][5], const mm_iir &f, int n) {
         for (int k = 0; k < 5; ++k) dst[s][k] = s < n ? f.sos[s][k] : 0.0;
 }
 
-template <int NS, bool P2>
-static int launch_eq_ch(mm_ctx *c, int ch, unsigned nb, const StageArgs &sa) {
-    const char *nm = P2 ? "eq_pass2" : "eq_pass1";
-    if (ch == 2) return launch(c, nm, eq_kernel<NS, P2, 2>, dim3(nb), dim3(256), 0, sa);
-    return launch(c, nm, eq_kernel<NS, P2, 1>, dim3(nb), dim3(256), 0, sa);
-}
-
-template <bool P2>
-static int launch_eq_p(mm_ctx *c, int nsec, int ch, unsigned nb, const StageArgs &sa) {
-    switch (nsec) {
-        case 1: return launch_eq_ch<1, P2>(c, ch, nb, sa);
-        case 2: return launch_eq_ch<2, P2>(c, ch, nb, sa);
-        case 3: return launch_eq_ch<3, P2>(c, ch, nb, sa);
-        default: return launch_eq_ch<4, P2>(c, ch, nb, sa);
+template <int NS>
+static int launch_eq_ns(mm_ctx *c, int ch, unsigned nblk, const EqArgs &ea, const LbArgs &lb, int64_t K) {
+    if (ch == 2) {
+        const size_t lds = eq_stage_bytes<2>() + lb_lds_bytes<2 * NS, 2>();
+        return launch(c, "eq", eq_kernel<NS, 2>, dim3(nblk), dim3(LB_THREADS), lds, ea, lb, K);
     }
+    const size_t lds = eq_stage_bytes<1>() + lb_lds_bytes<2 * NS, 1>();
+    return launch(c, "eq", eq_kernel<NS, 1>, dim3(nblk), dim3(LB_THREADS), lds, ea, lb, K);
 }
 
-static int launch_eq(mm_ctx *c, int nsec, bool pass2, int ch, unsigned nb, const StageArgs &sa) {
-    return pass2 ? launch_eq_p<true>(c, nsec, ch, nb, sa) : launch_eq_p<false>(c, nsec, ch, nb, sa);
+static int launch_eq(mm_ctx *c, int nsec, int ch, unsigned nblk, const EqArgs &ea, const LbArgs &lb, int64_t K) {
+    switch (nsec) {
+        case 1: return launch_eq_ns<1>(c, ch, nblk, ea, lb, K);
+        case 2: return launch_eq_ns<2>(c, ch, nblk, ea, lb, K);
+        case 3: return launch_eq_ns<3>(c, ch, nblk, ea, lb, K);
+        default: return launch_eq_ns<4>(c, ch, nblk, ea, lb, K);
+    }
 }
 
 // ------------------------------------------------------------ chain A..C
@@ -272,53 +256,62 @@ static int stage_chunks(mm_ctx *c, const mm_job *j, const float *d_in) {
     c->staged = false;
     short2 *q1;
     RET(get_buf(c, "q1", TG, &q1));
-    double *z8, *s8;
-    RET(get_buf(c, "z8", (size_t)std::max<int64_t>(G, 1) * ch * 8, &z8));
-    RET(get_buf(c, "s8", (size_t)std::max<int64_t>(G, 1) * ch * 8, &s8));
-    const unsigned nb = blocks_for(std::max<int64_t>(G, 1), 256);
+    RET(get_buf(c, "lb_error", 4, &c->lb_error));
+    HIPCHK(c, hipMemsetAsync(c->lb_error, 0, 4, c->stream));
+    const int tpb = LB_THREADS / ch;
+    const unsigned nblk = blocks_for(std::max<int64_t>(G, 1), tpb);
 
-    StageArgs sa{};
-    sa.in = d_in;
-    sa.N_in = j->frames_in;
-    sa.N_proc = N;
-    sa.G = G;
-    sa.T = T;
-    sa.ch = ch;
-    sa.sat.keep = j->sat_keep;
-    sa.sat.mix = j->sat_mix;
-    sa.sat.drive = j->sat_drive;
-    sa.sat.on = j->sat_on;
-    sa.width = j->width;
-    sa.width_on = j->width_on && ch == 2;
-    sa.z_out = z8;
-    sa.s_in = s8;
-    sa.q_out = q1;
+    EqArgs ea{};
+    ea.in = d_in;
+    ea.N_in = j->frames_in;
+    ea.N_proc = N;
+    ea.G = G;
+    ea.T = T;
+    ea.sat.keep = j->sat_keep;
+    ea.sat.mix = j->sat_mix;
+    ea.sat.drive = j->sat_drive;
+    ea.sat.on = j->sat_on;
+    ea.width = j->width;
+    ea.width_on = j->width_on && ch == 2;
+    ea.q_out = reinterpret_cast<int16_t *>(q1);
     if (G > 0) {
         // --- stage A: saturation -> EQ -> width -> int16 (AME:55-63)
         if (j->eq.nsec == 0) {
-            if (ch == 2) RET(launch(c, "pre_pointwise", pre_pointwise_kernel<2>, dim3(nb), dim3(256), 0, sa));
-            else RET(launch(c, "pre_pointwise", pre_pointwise_kernel<1>, dim3(nb), dim3(256), 0, sa));
+            const unsigned nf = blocks_for(N, 256);
+            if (ch == 2) RET(launch(c, "pre_pointwise", pre_pointwise_kernel<2>, dim3(nf), dim3(256), 0, ea));
+            else RET(launch(c, "pre_pointwise", pre_pointwise_kernel<1>, dim3(nf), dim3(256), 0, ea));
         } else {
-            fill_sos(sa.sos, j->eq, j->eq.nsec);
-            RET(launch_eq(c, j->eq.nsec, false, ch, nb, sa));
-            RET(run_scan(c, "eq_scan", j->eq, 8, ch, K, G, z8, s8, nullptr, nullptr));
-            RET(launch_eq(c, j->eq.nsec, true, ch, nb, sa));
+            fill_sos(ea.sos, j->eq, j->eq.nsec);
+            LbArgs lb{};
+            RET(upload_tables(c, "eq", j->eq, lb));
+            RET(lb_prepare(c, nblk, ch, lb));
+            RET(launch_eq(c, j->eq.nsec, ch, nblk, ea, lb, K));
         }
     }
     short2 *mix = q1;
+    const unsigned nb = blocks_for(std::max<int64_t>(G, 1), 256);
     if (j->multiband_on && G > 0) {
         // --- stage B: crossover + band quantisation (AME:196-206)
         short2 *bands[3];
         RET(get_buf(c, "band0", TG, &bands[0]));
         RET(get_buf(c, "band1", TG, &bands[1]));
         RET(get_buf(c, "band2", TG, &bands[2]));
-        StageArgs xa = sa;
+        XoArgs xa{};
+        xa.N_proc = N;
+        xa.G = G;
+        xa.T = T;
         fill_sos(xa.sos, j->xover, 4);
-        xa.q_in = q1;
-        for (int b = 0; b < 3; ++b) xa.band_out[b] = bands[b];
-        RET(launch(c, "xover_pass1", xover_kernel<false>, dim3(nb), dim3(256), 0, xa));
-        RET(run_scan(c, "xover_scan", j->xover, 8, ch, K, G, z8, s8, nullptr, nullptr));
-        RET(launch(c, "xover_pass2", xover_kernel<true>, dim3(nb), dim3(256), 0, xa));
+        xa.q_in = reinterpret_cast<const int16_t *>(q1);
+        for (int b = 0; b < 3; ++b) xa.band[b] = reinterpret_cast<int16_t *>(bands[b]);
+        LbArgs lb{};
+        RET(upload_tables(c, "xover", j->xover, lb));
+        RET(lb_prepare(c, nblk, ch, lb));
+        if (ch == 2)
+            RET(launch(c, "xover", xover_kernel<2>, dim3(nblk), dim3(LB_THREADS), lb_lds_bytes<8, 2>(), xa, lb,
+                       (int64_t)K));
+        else
+            RET(launch(c, "xover", xover_kernel<1>, dim3(nblk), dim3(LB_THREADS), lb_lds_bytes<8, 1>(), xa, lb,
+                       (int64_t)K));
 
         // --- stage C: 3-band compressor + overlay (AME:207-210)
         CompArgs ca{};
@@ -430,15 +423,22 @@ static int stage_chunks(mm_ctx *c, const mm_job *j, const float *d_in) {
     return MM_OK;
 }
 
+// Synchronises the stream and reports a look-back spin timeout (never expected:
+// every block only waits on blocks that started before it).
+static int check_lb_error(mm_ctx *c) {
+    unsigned e = 0;
+    if (c->lb_error) HIPCHK(c, hipMemcpyAsync(&e, c->lb_error, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (e) return set_err(c, MM_ERR_STATE, "IIR look-back timed out");
+    return MM_OK;
+}
+
 // ------------------------------------------------------------ K-weighting
 static int kweight_energies(mm_ctx *c, const double *carry_in_host, double *seg_host, double *range_end_host) {
     const mm_job *j = &c->job;
     const int64_t G = c->G;
-    const int T = j->tile;
-    double *z4, *s4, *part, *seg, *init = nullptr, *lend;
+    double *part, *seg, *lend;
     int64_t *part_seg, *bounds;
-    RET(get_buf(c, "z4", (size_t)std::max<int64_t>(G, 1) * 4, &z4));
-    RET(get_buf(c, "s4", (size_t)std::max<int64_t>(G, 1) * 4, &s4));
     RET(get_buf(c, "kw_part", (size_t)std::max<int64_t>(G, 1) * 2, &part));
     RET(get_buf(c, "kw_part_seg", (size_t)std::max<int64_t>(G, 1), &part_seg));
     RET(get_buf(c, "kw_seg", (size_t)j->n_segs, &seg));
@@ -446,36 +446,38 @@ static int kweight_energies(mm_ctx *c, const double *carry_in_host, double *seg_
     RET(get_buf(c, "kw_lend", 8, &lend));
     HIPCHK(c, hipMemcpyAsync(bounds, j->seg_bounds, (j->n_segs + 1) * sizeof(int64_t), hipMemcpyHostToDevice,
                              c->stream));
+    LbArgs lb{};
+    RET(upload_tables(c, "kweight", j->kweight, lb));
+    const unsigned nblk = blocks_for(G, LB_THREADS);
+    RET(lb_prepare(c, nblk, 1, lb));
     if (carry_in_host) {
+        double *init;
         RET(get_buf(c, "kw_init", 8, &init));
         HIPCHK(c, hipMemcpyAsync(init, carry_in_host, 4 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+        lb.init = init;
     }
     KwArgs ka{};
     ka.N_proc = j->frames_proc;
     ka.G = G;
-    ka.T = T;
+    ka.T = j->tile;
     ka.ch = j->channels;
-    for (int s = 0; s < 2; ++s)
-        for (int k = 0; k < 5; ++k) ka.sos[s][k] = j->kweight.sos[s][k];
-    ka.mix = c->mix;
-    ka.z_out = z4;
-    ka.s_in = s4;
+    for (int s_ = 0; s_ < 2; ++s_)
+        for (int k = 0; k < 5; ++k) ka.sos[s_][k] = j->kweight.sos[s_][k];
+    ka.mix = reinterpret_cast<const int16_t *>(c->mix);
     ka.n_segs = j->n_segs;
     ka.seg_bounds = bounds;
     ka.part = part;
     ka.part_seg = part_seg;
-    const unsigned nb = blocks_for(G, 256);
-    RET(launch(c, "kw_pass1", kweight_kernel<false>, dim3(nb), dim3(256), 0, ka));
-    RET(run_scan(c, "kw_scan", j->kweight, 4, 1, G, G, z4, s4, init, lend));
+    ka.line_end = range_end_host ? lend : nullptr;
+    RET(launch(c, "kweight", kweight_kernel, dim3(nblk), dim3(LB_THREADS), lb_lds_bytes<4, 1>(), ka, lb));
     if (range_end_host) {
         HIPCHK(c, hipMemcpyAsync(range_end_host, lend, 4 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
+        RET(check_lb_error(c));
         return MM_OK;
     }
-    RET(launch(c, "kw_pass2", kweight_kernel<true>, dim3(nb), dim3(256), 0, ka));
     RET(launch(c, "seg_reduce", seg_reduce_kernel, dim3(blocks_for(j->n_segs, 256)), dim3(256), 0, ka, seg));
     HIPCHK(c, hipMemcpyAsync(seg_host, seg, j->n_segs * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    RET(check_lb_error(c));
     return MM_OK;
 }
 
@@ -544,6 +546,7 @@ static int master_device(mm_ctx *c, const mm_job *j, const float *d_in, void *d_
         use_gain = 1;
     }
     RET(finalize(c, gain, use_gain, d_out));
+    if (!j->lufs_on) RET(check_lb_error(c));
     if (res) {
         res->loudness = L;
         res->gain_linear = gain;

@@ -24,8 +24,6 @@ import numpy as np
 import scipy.signal
 
 MAX_DIM = 8
-SCAN_POWERS = 12
-SCAN_THREADS = 1024
 CHUNK_MS = 30 * 1000  # AME:48
 DEFAULT_TILE = 125     # divides 30 s chunks at every rate that is a multiple of 25 Hz
 
@@ -191,27 +189,24 @@ def transition_matrix(sections, branches):
     return A
 
 
-SCAN_BLOCK = 256  # tiles per block of the block-local scan
+LB_THREADS = 256  # threads per block of the single-pass IIR kernels (csrc/lookback.h)
+TILE_POW, BLK_POW = 8, 65
 
 
-def _doublings(M, n):
-    out = [M]
-    for _ in range(n - 1):
-        out.append(out[-1] @ out[-1])
-    return np.stack(out)
-
-
-def scan_tables(A, tile, total_tiles, last_len):
-    """Transition powers for the three-level tile scan (csrc/scan.hip):
-    phi = A^T, pow2[k] = phi^(2^k), blk = phi^256, blk_pow[k] = blk^(c 2^k) with
-    c = blocks per thread of the block-carry scan, last = A^last_len."""
-    nblk = max(1, -(-total_tiles // SCAN_BLOCK))
-    c = max(1, -(-nblk // SCAN_THREADS))
+def lookback_tables(A, tile, tpb):
+    """Transition powers for the in-kernel tile carry (csrc/lookback.h):
+    tile_pow[k] = Phi_T^(2^k) with Phi_T = A^tile (block-local Kogge-Stone and
+    the per-tile carry application), blk_pow[e] = Phi_B^e with Phi_B = Phi_T^tpb
+    (decoupled look-back over up to 64 predecessor blocks per window)."""
     phi = np.linalg.matrix_power(A, tile)
-    blk = np.linalg.matrix_power(phi, SCAN_BLOCK)
-    return {"c": c, "phi": phi, "pow2": _doublings(phi, SCAN_POWERS), "blk": blk,
-            "blk_pow": _doublings(np.linalg.matrix_power(blk, c), SCAN_POWERS),
-            "last": np.linalg.matrix_power(A, last_len)}
+    tp = [phi]
+    for _ in range(TILE_POW - 1):
+        tp.append(tp[-1] @ tp[-1])
+    pb = np.linalg.matrix_power(phi, tpb)
+    bp = [np.eye(A.shape[0])]
+    for _ in range(BLK_POW - 1):
+        bp.append(bp[-1] @ pb)
+    return {"tile_pow": np.stack(tp), "blk_pow": np.stack(bp)}
 
 
 # ------------------------------------------------ compressor (pydub constants)

@@ -10,6 +10,7 @@ IO instead of GCS; `params` uses the worker's settings keys and defaults
 from __future__ import annotations
 
 import ctypes
+import functools
 import os
 
 import numpy as np
@@ -81,13 +82,13 @@ class Job:
         j.out_kind = out_kind
         G = -(-self.frames_proc // self.tile) if self.frames_proc else 0
         self.G = G
-        last_len = self.frames_proc - (G - 1) * self.tile if G else self.tile
+        tpb = design.LB_THREADS // self.channels  # stereo stages run lane pairs
         # --- EQ (1 branch)
         eq = design.eq_sections(self.rate, params)
-        self._fill_iir(j.eq, eq, [len(eq)], max(G, 1), self.tile, last_len)
+        self._fill_iir(j.eq, eq, [len(eq)], self.tile, tpb)
         # --- crossover (2 branches of 2)
         if multiband:
-            self._fill_iir(j.xover, design.crossover_sections(self.rate), [2, 2], max(G, 1), self.tile, last_len)
+            self._fill_iir(j.xover, design.crossover_sections(self.rate), [2, 2], self.tile, tpb)
             self._tables = []
             for b in range(3):
                 tk, td, rk, rd = design.BAND_DEFAULTS[b]
@@ -107,7 +108,7 @@ class Job:
         j.comp_super = COMP_SUPER_FRAMES
         # --- loudness
         if lufs is not None:
-            self._fill_iir(j.kweight, design.kweight_sections(self.rate), [2], max(G, 1), self.tile, last_len)
+            self._fill_iir(j.kweight, design.kweight_sections(self.rate), [2], self.tile, design.LB_THREADS)
             if seg_bounds is None:
                 nb, lo, hi, segb, scale = design.loudness_blocks(self.frames_proc, self.rate)
             else:  # rank-local segments; blocks are gated over the whole track elsewhere
@@ -124,22 +125,28 @@ class Job:
         self.job = j
 
     @staticmethod
-    def _fill_iir(dst, sections, branches, total_tiles, tile, last_len=None):
+    @functools.lru_cache(maxsize=32)
+    def _tables(sections, branches, tile, tpb):
+        A = design.transition_matrix(list(sections), list(branches))
+        t = design.lookback_tables(A, tile, tpb)
+        return (np.ascontiguousarray(t["tile_pow"].reshape(design.TILE_POW, -1)),
+                np.ascontiguousarray(t["blk_pow"].reshape(design.BLK_POW, -1)))
+
+    @classmethod
+    def _fill_iir(cls, dst, sections, branches, tile, tpb):
         dst.nsec = len(sections)
         dst.nsec_branch0 = branches[0]
         dst.dim = 2 * len(sections)
+        dst.tpb = tpb
         for s, sec in enumerate(sections):
             for k in range(5):
                 dst.sos[s][k] = float(sec[k])
         if not sections:
             return
-        A = design.transition_matrix(sections, branches)
-        t = design.scan_tables(A, tile, total_tiles, last_len or tile)
-        dst.scan_c = t["c"]
-        for field, arr in (("phi", t["phi"]), ("phi_pow", t["pow2"]), ("phi_blk", t["blk"]),
-                           ("phi_blk_pow", t["blk_pow"]), ("phi_last", t["last"])):
-            a = np.ascontiguousarray(arr, dtype=np.float64)
-            ctypes.memmove(getattr(dst, field), a.ctypes.data, a.nbytes)
+        key = tuple(tuple(float(v) for v in sec) for sec in sections)
+        tp, bp = cls._tables(key, tuple(branches), int(tile), int(tpb))
+        ctypes.memmove(dst.phi_tile_pow, tp.ctypes.data, tp.nbytes)
+        ctypes.memmove(dst.phi_blk_pow, bp.ctypes.data, bp.nbytes)
 
 
 def _as_f32_interleaved(pcm: np.ndarray) -> np.ndarray:

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmastering_amd.so")
 
 MM_OUT_I16, MM_OUT_F32 = 0, 1
-MAX_DIM, SCAN_POWERS = 8, 12
+MAX_DIM, TILE_POW, BLK_POW = 8, 8, 65
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
 c_int64_p = ctypes.POINTER(ctypes.c_int64)
@@ -22,12 +22,9 @@ c_int64_p = ctypes.POINTER(ctypes.c_int64)
 
 class MMIir(ctypes.Structure):
     _fields_ = [("nsec", ctypes.c_int32), ("nsec_branch0", ctypes.c_int32), ("dim", ctypes.c_int32),
-                ("scan_c", ctypes.c_int32), ("sos", (ctypes.c_double * 5) * 4),
-                ("phi", ctypes.c_double * (MAX_DIM * MAX_DIM)),
-                ("phi_pow", (ctypes.c_double * (MAX_DIM * MAX_DIM)) * SCAN_POWERS),
-                ("phi_blk", ctypes.c_double * (MAX_DIM * MAX_DIM)),
-                ("phi_blk_pow", (ctypes.c_double * (MAX_DIM * MAX_DIM)) * SCAN_POWERS),
-                ("phi_last", ctypes.c_double * (MAX_DIM * MAX_DIM))]
+                ("tpb", ctypes.c_int32), ("sos", (ctypes.c_double * 5) * 4),
+                ("phi_tile_pow", (ctypes.c_double * (MAX_DIM * MAX_DIM)) * TILE_POW),
+                ("phi_blk_pow", (ctypes.c_double * (MAX_DIM * MAX_DIM)) * BLK_POW)]
 
 
 class MMBand(ctypes.Structure):
