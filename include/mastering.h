@@ -66,10 +66,13 @@ typedef struct mm_band {
     double attack_frames;    /* attack_ms * (rate/1000.0)                      */
     double release_frames;   /* release_ms * (rate/1000.0)                     */
     int32_t look;            /* int(attack_frames)                             */
-    int32_t r0;              /* smallest rms r with max_att[r] != 0 (32769: none) */
-    const double *max_att;   /* host table [32769]: max attenuation for rms r;
-                                immutable while the context holds it (uploaded
-                                once per distinct pointer)                     */
+    int32_t r0;              /* smallest rms r with M[r] != 0 (32769: none)     */
+    const double *lut;       /* host table [32769][4] per integer rms r:
+                                {M, M/attack_frames, M/release_frames, 0} with
+                                M = (1-1/ratio)*max(20*log(r/thr,10), 0) (0 if r
+                                == 0), all in Python float arithmetic.  Immutable
+                                while the context holds it (uploaded once per
+                                distinct pointer)                              */
 } mm_band;
 
 /* A mastering job for one track (geometry + settings, all host memory). */
@@ -97,7 +100,7 @@ typedef struct mm_job {
     mm_band band[3];         /* low / mid / high                                */
     int32_t comp_warmup;     /* >0: speculative warm-up over the previous super-tile */
     int32_t comp_max_iters;  /* cap on fix-up sweeps (exactness check)          */
-    int32_t comp_super;      /* active frames per super-tile of the envelope solve */
+    int32_t comp_super;      /* frames per super-tile of the envelope solve (rounded to whole tiles) */
     int32_t _pad2;
     /* loudness geometry (pyloudnorm integrated_loudness, block 0.4 s, step 0.1 s) */
     int64_t n_blocks;

@@ -116,8 +116,8 @@ struct CompArgs {
     int64_t SPC;               // super-tiles reserved per chunk = ceil(chunk frames / U)
     int64_t GS;                // super-tiles = chunks * SPC
     const short2 *band[3];
-    const double *max_att[3];  // device LUTs [32769]
-    uint32_t r0[3];            // smallest rms with max_att != 0 ("above threshold")
+    const double *lut[3];      // device tables [32769]: M per integer rms
+    uint32_t r0[3];            // smallest rms with M != 0 ("above threshold")
     int look[3];
     double attack_frames[3], release_frames[3];
     double rcp_attack[3], rcp_release[3];
@@ -125,9 +125,9 @@ struct CompArgs {
     int32_t *cnt[3];           // per tile: active frames
     int32_t *off[3];           // per tile: compacted index of its first active frame (in chunk)
     int32_t *total[3];         // per chunk: active frames
-    double *Mc[3];             // compacted max attenuation, super-tile-major [U][GS]
-    double *start[3];          // per-super-tile speculative start state
-    double *tstart[3];         // per-tile start state (recorded by the walks)
+    double *Mc[3];             // compacted M of active frames, super-tile-major [U + 1][GS]
+    double *start[3];          // per-super-tile start state
+    double *tstart[3];         // per-tile start state (comp_record)
     const double *end_in[3];
     double *end_out[3];
     unsigned int *changed;

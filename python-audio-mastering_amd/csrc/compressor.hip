@@ -2,28 +2,37 @@
 //
 // pydub compress_dynamic_range per band (restated in SURVEY.md Appendix A):
 //   rms_i  = audioop.rms over frames [max(chunk0, i-look), i)  (excludes i)
-//   M_i    = (1 - 1/ratio) * max(20 log10(rms_i / thr), 0)       (host table, exact)
+//   M_i    = (1 - 1/ratio) * max(20 log10(rms_i / thr), 0)
 //   att_i  = (rms_i > thr && att <= M_i) ? min(att + M_i/A, M_i) : max(att - M_i/R, 0)
 //   out_i  = floor(x_i * 10^(-att_i/20))  if att_i != 0
 // audioop.rms = (unsigned)sqrt(S/n) equals isqrt(S div n) for integer S and the n
-// seen here (tests/test_oracle.py), so rms is computed exactly with
-// integers.  M_i == 0 exactly when rms_i <= thr ("hold": att unchanged), and
-// rms_i > thr <=> rms_i >= r0 (M is monotone in rms), r0 from the host table.
+// seen here (tests/test_oracle.py), so rms is computed exactly with integers.
+// M depends on the integer rms only: the host tabulates it with Python's own
+// float expressions (design.max_att_table); M/A and M/R are correctly rounded
+// Markstein divisions on the device.  M == 0 exactly when rms <= thr (then att
+// is held).
 //
-// The att recurrence is sequential and non-linear.  It is solved EXACTLY:
-//  1. comp_rms     per tile: rms -> uint16 r (tile-major) + active-frame counts;
-//  2. comp_offsets per chunk: exclusive scan of the counts (compacted offsets);
-//  3. comp_compact per tile: M of every active frame, scattered into a compacted,
-//     super-tile-major array (hold frames are identity, so they vanish);
-//  4. comp_pass0   per super-tile (U active frames): speculative walk warmed up
-//     over the previous super-tile from att = 0; the first of a chunk is exact;
+// Frames with M == 0 are identities, so the recurrence only "sees" the active
+// frames; it is solved EXACTLY per (chunk, band) over the compacted sequence of
+// active frames, cut into super-tiles of U active frames:
+//  1. comp_rms     per (tile, band): uint16 rms per frame (tile-major) and the
+//                  tile's active-frame count;
+//  2. comp_offsets per (chunk, band): exclusive scan of the counts;
+//  3. comp_compact per (tile, band): M of every active frame, scattered into
+//                  the compacted super-tile-major array Mc[U][GS];
+//  4. comp_pass0   per super-tile: warm-up walk over the previous super-tile
+//                  from att = 0, then its own walk -> start, end (exact for the
+//                  first super-tile of a chunk, where att starts at 0);
 //  5. comp_fix     Jacobi sweeps: a super-tile whose start differs from its
-//     predecessor's end re-runs from it; at the fixed point every start is the
-//     true state (induction from the exact chunk start);
-//  6. comp_record  one more walk from the converged starts overwrites the
-//     compacted M with the exact att after every active frame;
-//  7. comp_tstart  per tile: att at its first frame (gathered from step 6);
-//  8. comp_apply   per tile: exact att from there, gains, audioop.mul, overlay.
+//                  predecessor's end re-walks from it; at the fixed point every
+//                  start is the true state (induction from the chunk start);
+//  6. comp_record  one walk from the converged starts overwrites Mc with the
+//                  att after every active frame; comp_tstart gathers each
+//                  tile's starting att from it;
+//  7. comp_apply   per (tile, band): exact trajectory, gains, audioop.mul,
+//                  overlay through LDS.
+// Sparse bands (the high band is active on ~0.1 % of pink-noise frames) thus
+// cost a few super-tiles per chunk, and dense ones ~frames/U.
 #include "common.h"
 
 namespace mm {
@@ -40,63 +49,69 @@ __device__ __forceinline__ uint32_t rms_exact(int64_t S, int64_t n, float inv_n)
     return n > 0 ? (uint32_t)r : 0u;
 }
 
-// tile-major address of timeline frame f
-__device__ __forceinline__ int64_t tm_index(int64_t f, int T, int64_t G) {
-    int64_t g = f / T;
-    return (f - g * T) * G + g;
-}
-
-// 1. rms per frame (uint16 r, tile-major) and active counts per tile.
-// grid: (ceil(G/256), 3 bands)
+// 1. rms per frame (uint16 r, tile-major).  grid: (ceil(G/256), 3 bands).  The
+// window [max(chunk0, f-look), f) slides one frame per step: + frame f-1 (this
+// lane's own previous frame), - frame f-1-look (up to ~4 tiles back: another
+// lane's data, coalesced across the wave).  Frame -> (tile, offset) arithmetic is
+// incremental: no 64-bit division per frame.
 __global__ void __launch_bounds__(256) comp_rms_kernel(CompArgs a) {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int b = blockIdx.y;
     if (g >= a.G) return;
     const short2 *x = a.band[b];
     const int look = a.look[b];
-    const uint32_t r0 = a.r0[b];
     const int T = a.T;
     const int64_t G = a.G;
     const int64_t f0 = g * T;
     const int64_t chunk0 = (g / a.K) * a.K * T;
     const int len = (int)min((int64_t)T, a.N_proc - f0);
     const int ch = a.ch;
+    // warm-up: S over [lo0, f0)
     const int64_t lo0 = max(chunk0, f0 - look);
-    const int wl = (int)(f0 - lo0);
+    const int64_t gw = lo0 / T;
+    const int nw = (int)(lo0 - gw * T);
     int64_t S = 0;
-    stream<8, 2, short2>(
-        wl, [&](int i) { return x[tm_index(lo0 + min(i, wl - 1), T, G)]; },
-        [&](short2 v) { S += frame_energy(v); });
+    for (int64_t gt = gw, n_first = nw; gt < g; ++gt, n_first = 0) {  // <= look/T + 1 tiles
+#pragma unroll 8
+        for (int n = (int)n_first; n < T; ++n) S += frame_energy(x[(int64_t)n * G + gt]);
+    }
+    // drop frames: d = f - look for f >= chunk0 + look; the first `skip` frames drop nothing
+    const int64_t d_first = max(f0 - look, chunk0);
+    const int skip = (int)(d_first - (f0 - look));
+    const int64_t gd = d_first / T;
+    const int nd = (int)(d_first - gd * T);
     uint16_t *R = a.r16[b];
-    int64_t cnt_frames = f0 - lo0;
-    float inv = cnt_frames > 0 ? 1.0f / (float)(cnt_frames * ch) : 0.f;
-    int64_t pf = f0;
-    int active = 0;
+    int64_t cnt = f0 - lo0;
+    float inv = cnt > 0 ? 1.0f / (float)(cnt * ch) : 0.f;
+    const uint32_t r0 = a.r0[b];
+    int i_proc = 0, active = 0;
     struct Pair {
         short2 in, drop;
     };
     stream<8, 3, Pair>(
         len,
         [&](int i) {
-            const int64_t f = f0 + min(i, len - 1);
-            const int64_t fd = max(f - look, chunk0);  // clamped; unused when < chunk0
+            i = min(i, len - 1);
             Pair p;
-            p.in = x[tm_index(f, T, G)];
-            p.drop = x[tm_index(fd, T, G)];
+            p.in = x[(int64_t)i * G + g];
+            int k = nd + max(i - skip, 0);  // < 2T
+            const int wrap = k >= T;
+            k -= wrap ? T : 0;
+            p.drop = x[(int64_t)k * G + gd + wrap];
             return p;
         },
         [&](Pair p) {
-            const uint32_t r = rms_exact(S, cnt_frames * ch, inv);
-            R[(pf - f0) * G + g] = (uint16_t)r;
+            const uint32_t r = rms_exact(S, cnt * ch, inv);
+            R[(int64_t)i_proc * G + g] = (uint16_t)r;
             active += r >= r0;
             S += frame_energy(p.in);
-            const bool full = pf - look >= chunk0;
-            S -= full ? frame_energy(p.drop) : 0;
-            if (!full) {
-                ++cnt_frames;
-                inv = 1.0f / (float)(cnt_frames * ch);
+            if (i_proc >= skip) {
+                S -= frame_energy(p.drop);
+            } else {
+                ++cnt;
+                inv = 1.0f / (float)(cnt * ch);
             }
-            ++pf;
+            ++i_proc;
         });
     a.cnt[b][g] = active;
 }
@@ -130,12 +145,6 @@ __global__ void __launch_bounds__(1024) comp_offsets_kernel(CompArgs a) {
     if (tid == 1023) a.total[b][blockIdx.x] = buf[1023];
 }
 
-// compacted index p of chunk c -> element address in the super-tile-major array
-__device__ __forceinline__ int64_t cm_index(const CompArgs &a, int64_t c, int32_t p) {
-    const int32_t k = p / a.U, o = p - k * a.U;
-    return (int64_t)o * a.GS + c * a.SPC + k;
-}
-
 // 3. scatter M of active frames into the compacted array.  grid (ceil(G/256), 3)
 __global__ void __launch_bounds__(256) comp_compact_kernel(CompArgs a) {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -143,11 +152,13 @@ __global__ void __launch_bounds__(256) comp_compact_kernel(CompArgs a) {
     if (g >= a.G) return;
     if (a.cnt[b][g] == 0) return;
     const uint16_t *R = a.r16[b];
-    const double *lut = a.max_att[b];
+    const double *lut = a.lut[b];
     const uint32_t r0 = a.r0[b];
     const int64_t c = g / a.K;
     const int len = (int)min((int64_t)a.T, a.N_proc - g * a.T);
-    int32_t p = a.off[b][g];
+    const int32_t p = a.off[b][g];
+    int32_t k = p / a.U, o = p - k * a.U;  // super-tile and row of the next active frame
+    const int64_t base = c * a.SPC;
     double *Mc = a.Mc[b];
     // inactive frames store into this lane's own padding slot (row U of the
     // array), so every store is unconditional and the pipeline stays counted
@@ -157,16 +168,19 @@ __global__ void __launch_bounds__(256) comp_compact_kernel(CompArgs a) {
         [&](uint16_t r) { return lut[r]; },
         [&](uint16_t r, double m) {
             const bool act = r >= r0;
-            double *dst = act ? Mc + cm_index(a, c, p) : dummy;
+            double *dst = act ? Mc + (int64_t)o * a.GS + base + k : dummy;
             *dst = m;
-            p += act;
+            if (act && ++o == a.U) {
+                o = 0;
+                ++k;
+            }
         });
 }
 
 // correctly rounded m / d given rd = RN(1/d) (Markstein; tests/test_oracle.py)
 __device__ __forceinline__ double div_cr(double m, double d, double rd) {
-    double q = m * rd;
-    double rem = fma(-q, d, m);
+    const double q = m * rd;
+    const double rem = fma(-q, d, m);
     return fma(rem, rd, q);
 }
 
@@ -183,20 +197,25 @@ __device__ __forceinline__ BandStep band_step(const CompArgs &a, int b) {
     return s;
 }
 
-// one envelope step; M == 0 (hold) leaves att unchanged exactly
+// One envelope step, exactly pydub's
+//   if rms > thr and att <= M: att = min(att + M/A, M)
+//   else:                      att = max(att - M/R, 0)
+// M == 0 (rms <= thr) leaves att unchanged (inc = dec = 0); M != 0 implies
+// rms > thr, so the rms test folds away.  min/max are v_min_f64/v_max_f64
+// (equal operands and signed zeros give the same observable att); the
+// divisions are correctly rounded and off the att chain.
 __device__ __forceinline__ double comp_step(double att, double M, const BandStep &bs) {
-    const double inc = div_cr(M, bs.A, bs.rA);  // off the att critical path
+    const double inc = div_cr(M, bs.A, bs.rA);
     const double dec = div_cr(M, bs.R, bs.rR);
-    double up = att + inc;
-    up = (M < up) ? M : up;
-    double dn = att - dec;
-    dn = (0.0 > dn) ? 0.0 : dn;
-    return (M != 0.0 && att <= M) ? up : dn;
+    const double up = fmin(att + inc, M);
+    const double dn = fmax(att - dec, 0.0);
+    return att <= M ? up : dn;
 }
 
 struct Super {
     int64_t c;        // chunk
     int32_t p0, len;  // compacted range [p0, p0+len)
+    bool last;        // last super-tile holding frames of its chunk
 };
 
 __device__ __forceinline__ Super super_of(const CompArgs &a, int b, int64_t s) {
@@ -206,11 +225,13 @@ __device__ __forceinline__ Super super_of(const CompArgs &a, int b, int64_t s) {
     const int32_t L = a.total[b][r.c];
     r.p0 = (int32_t)(k * a.U);
     r.len = (int32_t)max((int64_t)0, min((int64_t)a.U, (int64_t)L - r.p0));
+    r.last = r.p0 + r.len == L;
     return r;
 }
 
-// Walk the envelope over a super-tile's compacted frames (branch-free stream).
-// With STORE, overwrite each compacted M with the att after that frame.
+// Walk the envelope over a super-tile's compacted frames (branch-free
+// software-pipelined stream).  With STORE, overwrite each compacted M with the
+// att after that frame.
 template <bool STORE>
 __device__ __forceinline__ double comp_walk(double att, const CompArgs &a, int b, int64_t s, int len,
                                             const BandStep &bs) {
@@ -271,7 +292,13 @@ __global__ void __launch_bounds__(256) comp_record_kernel(CompArgs a) {
     comp_walk<true>(st.p0 > 0 ? a.start[b][s] : 0.0, a, b, s, st.len, band_step(a, b));
 }
 
-// 7. per tile: att at its first frame = att after compacted frame off-1 (0 if
+// compacted index p of chunk c -> element address in the super-tile-major array
+__device__ __forceinline__ int64_t cm_index(const CompArgs &a, int64_t c, int32_t p) {
+    const int32_t k = p / a.U, o = p - k * a.U;
+    return (int64_t)o * a.GS + c * a.SPC + k;
+}
+
+// 6b. per tile: att at its first frame = att after compacted frame off-1 (0 if
 // the chunk had no active frame before it).  grid (ceil(G/256), 3)
 __global__ void __launch_bounds__(256) comp_tstart_kernel(CompArgs a) {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -281,72 +308,83 @@ __global__ void __launch_bounds__(256) comp_tstart_kernel(CompArgs a) {
     a.tstart[b][g] = p > 0 ? a.Mc[b][cm_index(a, g / a.K, p - 1)] : 0.0;
 }
 
-// 8. per tile: exact trajectory from tstart; gains on the three band samples
-// (audioop.mul floor), overlay sat16(sat16(lo+mid)+hi) (AME:210) -> q2.
-__global__ void __launch_bounds__(256) comp_apply_kernel(CompArgs a) {
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= a.G) return;
-    BandStep bs[3];
-    double att[3];
-    const double *lut[3];
-    uint32_t r0[3];
-#pragma unroll
-    for (int b = 0; b < 3; ++b) {
-        bs[b] = band_step(a, b);
-        att[b] = a.tstart[b][g];
-        lut[b] = a.max_att[b];
-        r0[b] = a.r0[b];
-    }
+// 7. gains + overlay.  A block = 64 tiles x 3 bands: wave w runs band w's exact
+// trajectory from tstart for its 64 tiles (audioop.mul floor on both channels),
+// 8 frames at a time into LDS; then all 192 threads overlay
+// sat16(sat16(lo + mid) + hi) (AME:210) and store q2 coalesced.
+constexpr int APPLY_TILES = 64, APPLY_STEP = 8;
+
+// -att / 20, correctly rounded (Markstein with RN(1/20) = 0.05; checked
+// exhaustively on the attenuation range in tests/test_oracle.py)
+__device__ __forceinline__ double neg_div20(double att) {
+    const double q = -att * 0.05;
+    const double rem = fma(-q, 20.0, -att);
+    return fma(rem, 0.05, q);
+}
+
+__global__ void __launch_bounds__(192) comp_apply_kernel(CompArgs a) {
+    __shared__ short2 lds[3][APPLY_STEP][APPLY_TILES];
+    const int b = threadIdx.x / APPLY_TILES;
+    const int lane = threadIdx.x % APPLY_TILES;
     const int64_t G = a.G;
-    const int len = (int)min((int64_t)a.T, a.N_proc - g * a.T);
-    struct Fr {
-        uint16_t r[3];
-        short2 v[3];
+    const int64_t g0 = (int64_t)blockIdx.x * APPLY_TILES;
+    const int64_t g = g0 + lane;
+    const bool valid = g < G;
+    const int T = a.T;
+    const int len = valid ? (int)min((int64_t)T, a.N_proc - g * T) : 0;
+    const double *lut = a.lut[b];
+    const BandStep bs = band_step(a, b);
+    const uint16_t *R = a.r16[b];
+    const short2 *X = a.band[b];
+    double att = valid ? a.tstart[b][g] : 0.0;
+    uint16_t rn[APPLY_STEP];
+    short2 vn[APPLY_STEP];
+    auto prefetch = [&](int n0) {
+#pragma unroll
+        for (int j = 0; j < APPLY_STEP; ++j) {
+            const int n = min(n0 + j, max(len - 1, 0));
+            const int64_t idx = (int64_t)n * G + (valid ? g : 0);
+            rn[j] = R[idx];
+            vn[j] = X[idx];
+        }
     };
-    struct Ms {
-        double m[3];
-    };
-    int pn = 0;
-    stream2<4, 2, Fr, Ms>(
-        len,
-        [&](int i) {
-            Fr f;
-            const int64_t idx = (int64_t)min(i, len - 1) * G + g;
+    prefetch(0);
+    for (int n0 = 0; n0 < T; n0 += APPLY_STEP) {
+        short2 v[APPLY_STEP];
+        double m[APPLY_STEP];
 #pragma unroll
-            for (int b = 0; b < 3; ++b) {
-                f.r[b] = a.r16[b][idx];
-                f.v[b] = a.band[b][idx];
-            }
-            return f;
-        },
-        [&](const Fr &f) {
-            Ms s;
+        for (int j = 0; j < APPLY_STEP; ++j) {
+            v[j] = vn[j];
+            m[j] = lut[rn[j]];
+        }
+        if (n0 + APPLY_STEP < T) prefetch(n0 + APPLY_STEP);
 #pragma unroll
-            for (int b = 0; b < 3; ++b) s.m[b] = lut[b][f.r[b]];  // lut[r] == 0 for r < r0 (hold)
-            return s;
-        },
-        [&](const Fr &f, const Ms &ms) {
-            int32_t accl = 0, accr = 0;
-#pragma unroll
-            for (int b = 0; b < 3; ++b) {
-                att[b] = comp_step(att[b], ms.m[b], bs[b]);
-                short2 s = f.v[b];
-                if (att[b] != 0.0) {
-                    const double gain = exp10(-att[b] / 20.0);
+        for (int j = 0; j < APPLY_STEP; ++j) {
+            if (n0 + j < len) {
+                att = comp_step(att, m[j], bs);
+                short2 s = v[j];
+                if (att != 0.0) {
+                    const double gain = exp10(neg_div20(att));  // db_to_float(-att)
                     s.x = audioop_mul(s.x, gain);
                     s.y = audioop_mul(s.y, gain);
                 }
-                if (b == 0) {
-                    accl = s.x;
-                    accr = s.y;
-                } else {
-                    accl = sat16(accl + s.x);
-                    accr = sat16(accr + s.y);
-                }
+                lds[b][j][lane] = s;
             }
-            a.q_out[(int64_t)(pn++) * G + g] =
-                make_short2((int16_t)accl, a.ch == 2 ? (int16_t)accr : (int16_t)0);
-        });
+        }
+        __syncthreads();
+        for (int p = threadIdx.x; p < APPLY_STEP * APPLY_TILES; p += 3 * APPLY_TILES) {
+            const int j = p / APPLY_TILES, tl = p % APPLY_TILES;
+            const int64_t gt = g0 + tl;
+            const int n = n0 + j;
+            if (gt < G && n < (int)min((int64_t)T, a.N_proc - gt * T)) {
+                const short2 lo = lds[0][j][tl], mi = lds[1][j][tl], hi = lds[2][j][tl];
+                const int16_t l = sat16(sat16((int32_t)lo.x + mi.x) + hi.x);
+                const int16_t rr = sat16(sat16((int32_t)lo.y + mi.y) + hi.y);
+                a.q_out[(int64_t)n * G + gt] = make_short2(l, a.ch == 2 ? rr : (int16_t)0);
+            }
+        }
+        __syncthreads();
+    }
 }
 
 }  // namespace mm

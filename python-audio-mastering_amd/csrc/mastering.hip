@@ -55,7 +55,7 @@ struct mm_ctx {
     std::map<std::string, KStat> stats;
     std::vector<std::string> stat_order;
     // host tables already resident on the device
-    const double *lut_src[3] = {nullptr, nullptr, nullptr};
+    const double *lut_src[3] = {nullptr, nullptr, nullptr};  // host tables already on the device
     std::map<std::string, std::vector<double>> mats_cache;
     // rccl
     ncclComm_t comm = nullptr;
@@ -203,8 +203,10 @@ static int validate(mm_ctx *c, const mm_job *j) {
     if (j->multiband_on) {
         if (j->xover.nsec != 4 || j->xover.nsec_branch0 != 2) return set_err(c, MM_ERR_ARG, "crossover must be 2+2 sections");
         for (int b = 0; b < 3; ++b) {
-            if (!j->band[b].max_att) return set_err(c, MM_ERR_ARG, "band %d: missing max_att table", b);
+            if (!j->band[b].lut) return set_err(c, MM_ERR_ARG, "band %d: missing table", b);
             if (j->band[b].look < 0) return set_err(c, MM_ERR_ARG, "band %d: look < 0", b);
+            if (!(j->band[b].release_frames >= 1.0) || !(j->band[b].attack_frames > 0.0))
+                return set_err(c, MM_ERR_ARG, "band %d: release must span >= 1 frame", b);
         }
     }
     if (j->lufs_on) {
@@ -325,14 +327,14 @@ static int stage_chunks(mm_ctx *c, const mm_job *j, const float *d_in) {
         const int64_t nchunks = (G + K - 1) / K;
         ca.SPC = ((int64_t)K * T + ca.U - 1) / ca.U;
         ca.GS = nchunks * ca.SPC;
-        const int64_t GS = ca.GS;
+        const int64_t NS = ca.GS;
         short2 *q2;
         RET(get_buf(c, "q2", TG, &q2));
         ca.q_out = q2;
-        double *st, *eA, *eB, *luts, *tst;
-        RET(get_buf(c, "comp_start", (size_t)3 * GS, &st));
-        RET(get_buf(c, "comp_endA", (size_t)3 * GS, &eA));
-        RET(get_buf(c, "comp_endB", (size_t)3 * GS, &eB));
+        double *st, *eA, *eB, *tst, *luts;
+        RET(get_buf(c, "comp_start", (size_t)3 * NS, &st));
+        RET(get_buf(c, "comp_endA", (size_t)3 * NS, &eA));
+        RET(get_buf(c, "comp_endB", (size_t)3 * NS, &eB));
         RET(get_buf(c, "comp_tstart", (size_t)3 * G, &tst));
         RET(get_buf(c, "comp_lut", (size_t)3 * 32769, &luts));
         unsigned int *changed;
@@ -347,17 +349,19 @@ static int stage_chunks(mm_ctx *c, const mm_job *j, const float *d_in) {
             char nm[16];
             snprintf(nm, sizeof nm, "comp_r%d", b);
             RET(get_buf(c, nm, TG, &rb));
-            snprintf(nm, sizeof nm, "comp_Mc%d", b);
-            RET(get_buf(c, nm, (size_t)GS * (ca.U + 1), &mcb));  // + one padding row
+            snprintf(nm, sizeof nm, "comp_mc%d", b);
+            RET(get_buf(c, nm, (size_t)NS * (ca.U + 1), &mcb));  // + one padding row
             ca.r16[b] = rb;
             ca.Mc[b] = mcb;
             ca.band[b] = bands[b];
-            ca.max_att[b] = luts + (size_t)b * 32769;
+            ca.lut[b] = luts + (size_t)b * 32769;
             // tables are immutable host arrays owned by the caller's job: upload once
-            if (c->lut_src[b] != j->band[b].max_att) {
-                HIPCHK(c, hipMemcpyAsync(luts + (size_t)b * 32769, j->band[b].max_att, 32769 * sizeof(double),
-                                         hipMemcpyHostToDevice, c->stream));
-                c->lut_src[b] = j->band[b].max_att;
+            if (c->lut_src[b] != j->band[b].lut) {
+                // the M column of the host's {M, M/A, M/R, 0} rows
+                HIPCHK(c, hipMemcpy2DAsync(luts + (size_t)b * 32769, sizeof(double), j->band[b].lut,
+                                           4 * sizeof(double), sizeof(double), 32769, hipMemcpyHostToDevice,
+                                           c->stream));
+                c->lut_src[b] = j->band[b].lut;
             }
             ca.r0[b] = (uint32_t)j->band[b].r0;
             ca.look[b] = j->band[b].look;
@@ -368,35 +372,34 @@ static int stage_chunks(mm_ctx *c, const mm_job *j, const float *d_in) {
             ca.cnt[b] = cnt + (size_t)b * G;
             ca.off[b] = off + (size_t)b * G;
             ca.total[b] = tot + (size_t)b * nchunks;
-            ca.start[b] = st + (size_t)b * GS;
+            ca.start[b] = st + (size_t)b * NS;
             ca.tstart[b] = tst + (size_t)b * G;
-            ca.end_out[b] = eA + (size_t)b * GS;
+            ca.end_out[b] = eA + (size_t)b * NS;
         }
-        const unsigned nbs = blocks_for(GS, 256);
+        const unsigned nbs = blocks_for(NS, 256);
         RET(launch(c, "comp_rms", comp_rms_kernel, dim3(nb, 3), dim3(256), 0, ca));
         RET(launch(c, "comp_offsets", comp_offsets_kernel, dim3((unsigned)nchunks, 3), dim3(1024), 0, ca));
         RET(launch(c, "comp_compact", comp_compact_kernel, dim3(nb, 3), dim3(256), 0, ca));
         RET(launch(c, "comp_pass0", comp_pass0_kernel, dim3(nbs, 3), dim3(256), 0, ca));
         // Jacobi sweeps queued in batches: sweep k writes flag k, and exits at once
         // if sweep k-1 changed nothing; one host sync per batch.
-        const int batch = 16;
-        int iters = 0;
+        int iters = 0, batch = 8;
         double *cur = eA, *nxt = eB;
         bool done = false;
         while (!done) {
-            HIPCHK(c, hipMemsetAsync(changed, 0, batch * sizeof(unsigned int), c->stream));
+            HIPCHK(c, hipMemsetAsync(changed, 0, 16 * sizeof(unsigned int), c->stream));
             for (int k = 0; k < batch; ++k) {
                 for (int b = 0; b < 3; ++b) {
-                    ca.end_in[b] = cur + (size_t)b * GS;
-                    ca.end_out[b] = nxt + (size_t)b * GS;
+                    ca.end_in[b] = cur + (size_t)b * NS;
+                    ca.end_out[b] = nxt + (size_t)b * NS;
                 }
                 ca.changed = changed + k;
                 const unsigned int *prevf = k > 0 ? changed + (k - 1) : nullptr;
                 RET(launch(c, "comp_fix", comp_fix_kernel, dim3(nbs, 3), dim3(256), 0, ca, prevf));
                 std::swap(cur, nxt);
             }
-            unsigned int h[batch];
-            HIPCHK(c, hipMemcpyAsync(h, changed, sizeof h, hipMemcpyDeviceToHost, c->stream));
+            unsigned int h[16];
+            HIPCHK(c, hipMemcpyAsync(h, changed, batch * sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream));
             HIPCHK(c, hipStreamSynchronize(c->stream));
             for (int k = 0; k < batch; ++k) {
                 if (h[k] == 0) {
@@ -409,11 +412,13 @@ static int stage_chunks(mm_ctx *c, const mm_job *j, const float *d_in) {
             }
             if (!done && iters >= j->comp_max_iters)
                 return set_err(c, MM_ERR_STATE, "compressor did not converge in %d sweeps", iters);
+            batch = 4;
         }
         c->job.comp_max_iters = iters;  // reported via mm_result
         RET(launch(c, "comp_record", comp_record_kernel, dim3(nbs, 3), dim3(256), 0, ca));
         RET(launch(c, "comp_tstart", comp_tstart_kernel, dim3(nb, 3), dim3(256), 0, ca));
-        RET(launch(c, "comp_apply", comp_apply_kernel, dim3(nb), dim3(256), 0, ca));
+        RET(launch(c, "comp_apply", comp_apply_kernel, dim3(blocks_for(G, APPLY_TILES)), dim3(3 * APPLY_TILES), 0,
+                   ca));
         mix = q2;
     } else {
         c->job.comp_max_iters = 0;

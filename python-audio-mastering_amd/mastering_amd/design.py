@@ -231,11 +231,26 @@ def max_att_table(threshold, ratio):
     return out, thresh_rms
 
 
+@functools.lru_cache(maxsize=64)
+def step_table(threshold, ratio, attack_frames, release_frames):
+    """Per integer rms r: {M, M/attack_frames, M/release_frames, 0} — the three
+    numbers pydub's loop derives from rms_at(i) (max_attenuation,
+    attenuation_inc, attenuation_dec), each a correctly rounded Python float."""
+    M, _ = max_att_table(threshold, ratio)
+    out = np.zeros((32769, 4), np.float64)
+    out[:, 0] = M
+    out[:, 1] = M / attack_frames   # numpy float64 division: IEEE, correctly rounded
+    out[:, 2] = M / release_frames
+    out.setflags(write=False)
+    return out
+
+
 def band_constants(rate, threshold, ratio, attack, release):
     table, thr = max_att_table(float(threshold), float(ratio))
     af = attack * (rate / 1000.0)
     rf = release * (rate / 1000.0)
-    return {"table": table, "thresh_rms": thr, "attack_frames": af, "release_frames": rf, "look": int(af)}
+    return {"table": table, "thresh_rms": thr, "attack_frames": af, "release_frames": rf, "look": int(af),
+            "lut": step_table(float(threshold), float(ratio), af, rf)}
 
 
 # ---------------------------------------------------- loudness block geometry

@@ -31,7 +31,8 @@ EQ_PRESETS = {
 
 COMP_WARMUP = 1          # warm up each super-tile over its predecessor
 COMP_MAX_ITERS = 100000
-COMP_SUPER_FRAMES = 1000  # envelope solve unit (frames) -> ~8 Jacobi sweeps on pink noise
+# envelope solve unit (active frames) -> ~8 Jacobi sweeps on pink noise; MM_COMP_SUPER overrides
+COMP_SUPER_FRAMES = int(os.environ.get("MM_COMP_SUPER", "1000"))
 
 
 class Job:
@@ -94,15 +95,15 @@ class Job:
                 tk, td, rk, rd = design.BAND_DEFAULTS[b]
                 at, rel = design.BAND_TIMES[b]
                 bc = design.band_constants(self.rate, params.get(tk, td), params.get(rk, rd), at, rel)
-                tab = np.ascontiguousarray(bc["table"])
+                tab = np.ascontiguousarray(bc["lut"])
                 self._tables.append(tab)
                 jb = j.band[b]
                 jb.thresh_rms, jb.attack_frames, jb.release_frames = bc["thresh_rms"], bc["attack_frames"], \
                     bc["release_frames"]
                 jb.look = bc["look"]
-                nz = np.flatnonzero(tab)
+                nz = np.flatnonzero(tab[:, 0])
                 jb.r0 = int(nz[0]) if nz.size else 32769
-                jb.max_att = tab.ctypes.data_as(native.c_double_p)
+                jb.lut = tab.ctypes.data_as(native.c_double_p)
         j.comp_warmup = COMP_WARMUP
         j.comp_max_iters = COMP_MAX_ITERS
         j.comp_super = COMP_SUPER_FRAMES

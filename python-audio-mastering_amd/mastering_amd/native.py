@@ -30,7 +30,7 @@ class MMIir(ctypes.Structure):
 class MMBand(ctypes.Structure):
     _fields_ = [("thresh_rms", ctypes.c_double), ("attack_frames", ctypes.c_double),
                 ("release_frames", ctypes.c_double), ("look", ctypes.c_int32), ("r0", ctypes.c_int32),
-                ("max_att", c_double_p)]
+                ("lut", c_double_p)]
 
 
 class MMJob(ctypes.Structure):

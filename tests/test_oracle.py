@@ -120,3 +120,34 @@ def test_markstein_division():
             e = fma(-q, d, M)
             q2 = fma(e, r, q)
             assert q2 == M / d
+
+
+def test_neg_div20_markstein():
+    """comp_apply computes pydub's db_to_float(-att) argument -att/20 as
+    q = -att*0.05; r = fma(-q, 20, -att); q + r*0.05 (csrc/compressor.hip):
+    equal to the correctly rounded quotient (checked with exact rationals)."""
+    from fractions import Fraction
+    rng = np.random.default_rng(2)
+
+    def fma(a, b, c):
+        return float(Fraction(a) * Fraction(b) + Fraction(c))
+
+    atts = np.concatenate([rng.uniform(0, 40, 4000), rng.uniform(0, 1e-3, 500), [0.0, 1.0, 20.0, 1e-300]])
+    for att in atts:
+        q = -att * 0.05
+        r = fma(-q, 20.0, -att)
+        assert fma(r, 0.05, q) == -att / 20.0, att
+
+
+def test_step_table_matches_pydub_floats():
+    """The device step table {M, M/A, M/R} equals pydub's per-frame float math."""
+    from mastering_amd import design
+    for (thr, ratio), (at, rel) in zip(((-25.0, 6.0), (-20.0, 3.0), (-15.0, 4.0)), design.BAND_TIMES):
+        for rate in (44100, 96000):
+            bc = design.band_constants(rate, thr, ratio, at, rel)
+            lut, A, R = bc["lut"], bc["attack_frames"], bc["release_frames"]
+            thresh = 32768.0 * 10 ** (thr / 20)
+            for r in (0, 1, 500, int(thresh), int(thresh) + 1, 5000, 32767, 32768):
+                dbo = 0.0 if r == 0 else max(20 * math.log(r / thresh, 10), 0)
+                M = (1 - 1.0 / ratio) * dbo
+                assert lut[r, 0] == M and lut[r, 1] == M / A and lut[r, 2] == M / R

@@ -1,0 +1,82 @@
+// Microbenchmark: cycles per envelope step for one lane, by formulation.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#pragma clang fp contract(off)
+__device__ __forceinline__ double div_cr(double m, double d, double rd) {
+    double q = m * rd; double rem = fma(-q, d, m); return fma(rem, rd, q);
+}
+template <int V>
+__device__ __forceinline__ double step(double att, double M, double inc, double dec) {
+    if (V == 0) {  // min/max
+        double up = fmin(att + inc, M), dn = fmax(att - dec, 0.0);
+        return att <= M ? up : dn;
+    } else if (V == 1) {  // selects, no clamp at 0 (provably inactive)
+        double t = att + inc, d = att - dec;
+        double up = (M < t) ? M : t;
+        return att <= M ? up : d;
+    } else {  // min without canonicalize via integer compare of non-negative doubles
+        double t = att + inc, d = att - dec;
+        double up = fmin(t, M);
+        return att <= M ? up : d;
+    }
+}
+template <int V, int CHAINS>
+__global__ void bench(const double* in, int n, double* out, long long* cyc) {
+    if (threadIdx.x != 0) return;
+    double att[CHAINS];
+    for (int c = 0; c < CHAINS; ++c) att[c] = 0.1 * c;
+    double M[4], inc[4], dec[4];
+    for (int k = 0; k < 4; ++k) { M[k] = in[k]; inc[k] = div_cr(M[k], 441.0, 1.0/441.0); dec[k] = div_cr(M[k], 8820.0, 1.0/8820.0); }
+    long long t0 = clock64();
+    for (int i = 0; i < n; i += 4) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int c = 0; c < CHAINS; ++c) att[c] = step<V>(att[c], M[k], inc[k], dec[k]);
+    }
+    long long t1 = clock64();
+    double s = 0; for (int c = 0; c < CHAINS; ++c) s += att[c];
+    out[0] = s; cyc[0] = t1 - t0;
+}
+template <int CHAINS>
+__global__ void bench_div(const double* in, int n, double* out, long long* cyc) {
+    if (threadIdx.x != 0) return;
+    double att[CHAINS];
+    for (int c = 0; c < CHAINS; ++c) att[c] = 0.1 * c;
+    double M[4]; for (int k = 0; k < 4; ++k) M[k] = in[k];
+    long long t0 = clock64();
+    for (int i = 0; i < n; i += 4) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            double inc = div_cr(M[k], 441.0, 1.0/441.0), dec = div_cr(M[k], 8820.0, 1.0/8820.0);
+#pragma unroll
+            for (int c = 0; c < CHAINS; ++c) att[c] = step<0>(att[c], M[k], inc, dec);
+        }
+    }
+    long long t1 = clock64();
+    double s = 0; for (int c = 0; c < CHAINS; ++c) s += att[c];
+    out[0] = s; cyc[0] = t1 - t0;
+}
+template <class K>
+void run(const char* name, K k, const double* d, double* o, long long* c, int n, int chains) {
+    long long cy;
+    hipLaunchKernelGGL(k, 1, 64, 0, 0, d, n, o, c); hipDeviceSynchronize();
+    hipLaunchKernelGGL(k, 1, 64, 0, 0, d, n, o, c); hipDeviceSynchronize();
+    hipMemcpy(&cy, c, 8, hipMemcpyDeviceToHost);
+    printf("%-28s chains=%d  %.1f cycles/step/chain\n", name, chains, (double)cy / n / chains);
+}
+int main() {
+    double h[4] = {9.5, 9.6, 9.4, 9.55};
+    double *d, *o; long long *c;
+    hipMalloc(&d, 32); hipMalloc(&o, 8); hipMalloc(&c, 8);
+    hipMemcpy(d, h, 32, hipMemcpyHostToDevice);
+    const int n = 200000;
+    run("div_cr inline + minmax", bench_div<1>, d, o, c, n, 1);
+    run("div_cr inline + minmax", bench_div<2>, d, o, c, n, 2);
+    run("precomp minmax", bench<0, 1>, d, o, c, n, 1);
+    run("precomp selects", bench<1, 1>, d, o, c, n, 1);
+    run("precomp fmin, no clamp0", bench<2, 1>, d, o, c, n, 1);
+    run("precomp selects", bench<1, 2>, d, o, c, n, 2);
+    run("precomp selects", bench<1, 4>, d, o, c, n, 4);
+    return 0;
+}
