@@ -138,6 +138,7 @@ struct FinArgs {
     int64_t N_proc, G;
     int T, ch, out_kind, use_gain;
     double gain;
+    const double *gain_dev;  // device gain (loudness gated on the device) or null
     const short2 *mix;
     void *out;
 };

@@ -261,25 +261,69 @@ __global__ void __launch_bounds__(256) comp_pass0_kernel(CompArgs a) {
 }
 
 // 5. one Jacobi sweep (exits at once if the previous sweep changed nothing).
-__global__ void __launch_bounds__(256) comp_fix_kernel(CompArgs a, const unsigned int *prev_changed) {
+// grid: (ceil(GS/64), 3), one wave per block.  A lane whose start changed
+// re-walks its super-tile.  When only a few lanes of the wave walk (the later
+// sweeps, where only the chains of non-coalescing super-tiles remain), the whole
+// wave serves them one at a time: it loads the super-tile's M values and
+// computes M/A and M/R in parallel into LDS, then the walking lane runs the lean
+// step from LDS (~50 instead of ~130 cycles per step for a lone lane that also
+// divides; tools/micro/step_bench.hip).
+constexpr int FIX_COOP_MAX = 4;     // walkers per wave served cooperatively
+constexpr int FIX_MAX_U = 1024;     // LDS capacity (frames per super-tile)
+
+__global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned int *prev_changed) {
+    __shared__ double sm[FIX_MAX_U], si[FIX_MAX_U], sd[FIX_MAX_U];
     if (prev_changed && *prev_changed == 0u) return;
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x;
+    const int64_t s = (int64_t)blockIdx.x * 64 + lane;
     const int b = blockIdx.y;
-    if (s >= a.GS) return;
-    const Super st = super_of(a, b, s);
-    if (st.len == 0) return;
+    const bool valid = s < a.GS;
+    const Super st = valid ? super_of(a, b, s) : Super{0, 0, 0};
+    const bool live = valid && st.len > 0;
     const double *end_in = a.end_in[b];
-    double e = end_in[s];
-    if (st.p0 > 0) {
-        const double want = end_in[s - 1];
-        const double have = a.start[b][s];
-        if (__double_as_longlong(want) != __double_as_longlong(have)) {
-            e = comp_walk<false>(want, a, b, s, st.len, band_step(a, b));
-            a.start[b][s] = want;
-            *a.changed = 1u;  // benign race: every writer stores 1
+    double e = live ? end_in[s] : 0.0;
+    double want = 0.0;
+    bool need = false;
+    if (live && st.p0 > 0) {
+        want = end_in[s - 1];
+        need = __double_as_longlong(want) != __double_as_longlong(a.start[b][s]);
+    }
+    const BandStep bs = band_step(a, b);
+    unsigned long long m = __ballot(need);
+    if (__popcll(m) > FIX_COOP_MAX) {
+        if (need) e = comp_walk<false>(want, a, b, s, st.len, bs);
+    } else {
+        const double *Mc = a.Mc[b];
+        while (m) {  // wave-uniform
+            const int j = __builtin_ctzll(m);
+            m &= m - 1;
+            const int len = __shfl(st.len, j);
+            const int64_t sj = (int64_t)blockIdx.x * 64 + j;
+            for (int i = lane; i < len; i += 64) {
+                const double mv = Mc[(int64_t)i * a.GS + sj];
+                sm[i] = mv;
+                si[i] = div_cr(mv, bs.A, bs.rA);
+                sd[i] = div_cr(mv, bs.R, bs.rR);
+            }
+            __syncthreads();
+            if (lane == j) {
+                double att = want;
+#pragma unroll 8
+                for (int i = 0; i < len; ++i) {
+                    const double up = fmin(att + si[i], sm[i]);
+                    const double dn = fmax(att - sd[i], 0.0);
+                    att = att <= sm[i] ? up : dn;
+                }
+                e = att;
+            }
+            __syncthreads();
         }
     }
-    a.end_out[b][s] = e;
+    if (need) {
+        a.start[b][s] = want;
+        *a.changed = 1u;  // benign race: every writer stores 1
+    }
+    if (live) a.end_out[b][s] = e;
 }
 
 // 6. exact att after every active frame (Mc is overwritten in place).

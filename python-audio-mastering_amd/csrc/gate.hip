@@ -1,0 +1,91 @@
+// gate.hip — pyloudnorm's gated integrated loudness and the normalisation gain,
+// on the device, so the chain runs without a host round trip (AME:212-222).
+//
+// pyloudnorm 0.1.1 Meter.integrated_loudness (mono, channel gain 1):
+//   z_j   = (1/(0.4 rate)) * sum of K-weighted y^2 over block j (0.4 s, 0.1 s hop)
+//   l_j   = -0.691 + 10 log10(z_j)
+//   abs   : J_a = { j : l_j >= -70 }
+//   rel   : Gamma_r = -0.691 + 10 log10(mean_{J_a} z) - 10
+//   final : J_g = { j : l_j > Gamma_r and l_j > -70 },  L = -0.691 + 10 log10(mean_{J_g} z)
+//           (nan_to_num: an empty J_g gives z = 0 -> L = -inf)
+// AME:219-222: gain = 10 ** ((target - L) / 20).
+// Block energies are sums of the 0.1 s segment energies kweight_kernel produced;
+// the per-block sum runs in segment order like the host restatement
+// (mm_gate_loudness); the reductions over blocks are tree-ordered (the result
+// differs from a sequential sum in the last bits only).
+#include "common.h"
+
+namespace mm {
+
+struct GateArgs {
+    int64_t n_blocks;
+    const int32_t *blk_s0;  // first segment of block j
+    const int32_t *blk_s1;  // one past its last segment
+    const double *seg;      // segment energies
+    double scale;           // 1 / (0.4 rate)
+    double target;          // LUFS target
+    double *out;            // [0] = L, [1] = gain
+};
+
+constexpr int GATE_THREADS = 1024;
+
+__device__ __forceinline__ double gate_block_z(const GateArgs &a, int64_t j) {
+    double acc = 0.0;
+    for (int s = a.blk_s0[j]; s < a.blk_s1[j]; ++s) acc += a.seg[s];
+    return a.scale * acc;
+}
+
+// sum and count over the block (tree order), result broadcast to every thread
+__device__ __forceinline__ void gate_reduce(double &sum, long long &cnt, double *rs, long long *rc) {
+    const int t = threadIdx.x;
+    rs[t] = sum;
+    rc[t] = cnt;
+    __syncthreads();
+    for (int d = GATE_THREADS / 2; d > 0; d >>= 1) {
+        if (t < d) {
+            rs[t] += rs[t + d];
+            rc[t] += rc[t + d];
+        }
+        __syncthreads();
+    }
+    sum = rs[0];
+    cnt = rc[0];
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(GATE_THREADS) gate_kernel(GateArgs a) {
+    __shared__ double rs[GATE_THREADS];
+    __shared__ long long rc[GATE_THREADS];
+    const int t = threadIdx.x;
+    double sum = 0.0;
+    long long cnt = 0;
+    for (int64_t j = t; j < a.n_blocks; j += GATE_THREADS) {
+        const double z = gate_block_z(a, j);
+        if (-0.691 + 10.0 * log10(z) >= -70.0) {
+            sum += z;
+            ++cnt;
+        }
+    }
+    gate_reduce(sum, cnt, rs, rc);
+    const double mean_abs = cnt ? sum / (double)cnt : __longlong_as_double(0x7ff8000000000000LL);
+    const double gamma_r = -0.691 + 10.0 * log10(mean_abs) - 10.0;
+    sum = 0.0;
+    cnt = 0;
+    for (int64_t j = t; j < a.n_blocks; j += GATE_THREADS) {
+        const double z = gate_block_z(a, j);
+        const double l = -0.691 + 10.0 * log10(z);
+        if (l > gamma_r && l > -70.0) {
+            sum += z;
+            ++cnt;
+        }
+    }
+    gate_reduce(sum, cnt, rs, rc);
+    if (t == 0) {
+        const double zavg = cnt ? sum / (double)cnt : 0.0;
+        const double L = -0.691 + 10.0 * log10(zavg);
+        a.out[0] = L;
+        a.out[1] = pow(10.0, (a.target - L) / 20.0);
+    }
+}
+
+}  // namespace mm

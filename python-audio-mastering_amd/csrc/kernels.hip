@@ -65,6 +65,7 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
     __syncthreads();
     const int64_t f_base = g0 * T;
     const int64_t nf = min((int64_t)ntile * T, a.N_proc - f_base);
+    const double gain = a.gain_dev ? *a.gain_dev : a.gain;
     for (int64_t i = threadIdx.x; i < nf; i += blockDim.x) {
         int t = (int)(i / T), n = (int)(i - (int64_t)t * T);
         short2 q = lds[t * stride + n];
@@ -73,7 +74,7 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
         for (int c = 0; c < a.ch; ++c) {
             float y = (float)qq[c] / 32768.0f;
             if (a.use_gain) {
-                double v = (double)y * a.gain;
+                double v = (double)y * gain;
                 o[c] = quantize(limiter64(v));
             } else {
                 o[c] = quantize((double)limiter32(y));

@@ -15,6 +15,7 @@
 #include "iir.hip"
 #include "kernels.hip"
 #include "compressor.hip"
+#include "gate.hip"
 
 using namespace mm;
 
@@ -48,6 +49,18 @@ struct mm_ctx {
     int64_t G = 0;
     short2 *mix = nullptr;
     unsigned *lb_error = nullptr;
+    // compressor state kept across the queued launches (stage_front -> comp_sweeps/comp_back)
+    bool comp_on = false;
+    CompArgs ca{};
+    double *comp_cur = nullptr, *comp_nxt = nullptr;
+    unsigned *comp_changed = nullptr;
+    int comp_iters = 0, comp_pending = 0;
+    unsigned comp_nb = 0, comp_nbs = 0;
+    // loudness on the device
+    double *gate_out = nullptr;         // [2]: L, gain
+    std::vector<int64_t> geom_cache;    // loudness geometry already on the device
+    int32_t *blk_s0 = nullptr, *blk_s1 = nullptr;
+    int64_t *seg_bounds_dev = nullptr;
     // timing
     bool timing = false;
     std::vector<PendingEvent> pending;
@@ -246,8 +259,69 @@ static int launch_eq(mm_ctx *c, int nsec, int ch, unsigned nblk, const EqArgs &e
     }
 }
 
+// --------------------------------------------------- compressor sweeps
+// Jacobi sweeps are queued without a host sync: sweep k writes flag k and exits
+// at once if sweep k-1 changed nothing (so after the first quiet sweep both end
+// buffers hold the converged ends).  Convergence is checked at the chain's
+// single sync (comp_check); a rare unconverged batch is extended there.
+constexpr int COMP_SWEEPS = 12;
+
+static int comp_sweeps(mm_ctx *c, int n, bool resume = false) {
+    CompArgs &ca = c->ca;
+    // comp_record overwrote Mc with attenuations: restore M before resuming
+    if (resume) RET(launch(c, "comp_compact", comp_compact_kernel, dim3(c->comp_nb, 3), dim3(256), 0, ca));
+    const int64_t NS = ca.GS;
+    HIPCHK(c, hipMemsetAsync(c->comp_changed, 0, 16 * sizeof(unsigned int), c->stream));
+    for (int k = 0; k < n; ++k) {
+        for (int b = 0; b < 3; ++b) {
+            ca.end_in[b] = c->comp_cur + (size_t)b * NS;
+            ca.end_out[b] = c->comp_nxt + (size_t)b * NS;
+        }
+        ca.changed = c->comp_changed + k;
+        const unsigned int *prevf = k > 0 ? c->comp_changed + (k - 1) : nullptr;
+        RET(launch(c, "comp_fix", comp_fix_kernel, dim3(blocks_for(NS, 64), 3), dim3(64), 0, ca, prevf));
+        std::swap(c->comp_cur, c->comp_nxt);
+    }
+    c->comp_pending = n;
+    return MM_OK;
+}
+
+// att at every tile start from the converged super-tile starts, then gains +
+// overlay into q2.
+static int comp_back(mm_ctx *c) {
+    const CompArgs &ca = c->ca;
+    RET(launch(c, "comp_record", comp_record_kernel, dim3(c->comp_nbs, 3), dim3(256), 0, ca));
+    RET(launch(c, "comp_tstart", comp_tstart_kernel, dim3(c->comp_nb, 3), dim3(256), 0, ca));
+    return launch(c, "comp_apply", comp_apply_kernel, dim3(blocks_for(ca.G, APPLY_TILES)), dim3(3 * APPLY_TILES), 0,
+                  ca);
+}
+
+// Synchronises the stream; reports look-back timeouts (never expected: a block
+// only waits on blocks that started before it) and whether the queued sweeps
+// converged.
+static int chain_check(mm_ctx *c, bool *converged) {
+    unsigned e = 0, flags[16] = {0};
+    if (c->lb_error) HIPCHK(c, hipMemcpyAsync(&e, c->lb_error, 4, hipMemcpyDeviceToHost, c->stream));
+    if (c->comp_on && c->comp_pending)
+        HIPCHK(c, hipMemcpyAsync(flags, c->comp_changed, c->comp_pending * sizeof(unsigned), hipMemcpyDeviceToHost,
+                                 c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (e) return set_err(c, MM_ERR_STATE, "IIR look-back timed out");
+    *converged = true;
+    if (c->comp_on && c->comp_pending) {
+        int k = 0;
+        while (k < c->comp_pending && flags[k]) ++k;
+        c->comp_iters += k;
+        *converged = k < c->comp_pending;
+        c->comp_pending = 0;
+        if (!*converged && c->comp_iters >= c->job.comp_max_iters)
+            return set_err(c, MM_ERR_STATE, "compressor did not converge in %d sweeps", c->comp_iters);
+    }
+    return MM_OK;
+}
+
 // ------------------------------------------------------------ chain A..C
-static int stage_chunks(mm_ctx *c, const mm_job *j, const float *d_in) {
+static int stage_front(mm_ctx *c, const mm_job *j, const float *d_in) {
     RET(validate(c, j));
     const int T = j->tile, ch = j->channels, K = j->tiles_per_chunk;
     const int64_t N = j->frames_proc;
@@ -323,7 +397,7 @@ static int stage_chunks(mm_ctx *c, const mm_job *j, const float *d_in) {
         ca.K = K;
         ca.ch = ch;
         ca.warmup = j->comp_warmup;
-        ca.U = std::max(16, j->comp_super);
+        ca.U = std::max(16, std::min(j->comp_super, FIX_MAX_U));
         const int64_t nchunks = (G + K - 1) / K;
         ca.SPC = ((int64_t)K * T + ca.U - 1) / ca.U;
         ca.GS = nchunks * ca.SPC;
@@ -381,76 +455,69 @@ static int stage_chunks(mm_ctx *c, const mm_job *j, const float *d_in) {
         RET(launch(c, "comp_offsets", comp_offsets_kernel, dim3((unsigned)nchunks, 3), dim3(1024), 0, ca));
         RET(launch(c, "comp_compact", comp_compact_kernel, dim3(nb, 3), dim3(256), 0, ca));
         RET(launch(c, "comp_pass0", comp_pass0_kernel, dim3(nbs, 3), dim3(256), 0, ca));
-        // Jacobi sweeps queued in batches: sweep k writes flag k, and exits at once
-        // if sweep k-1 changed nothing; one host sync per batch.
-        int iters = 0, batch = 8;
-        double *cur = eA, *nxt = eB;
-        bool done = false;
-        while (!done) {
-            HIPCHK(c, hipMemsetAsync(changed, 0, 16 * sizeof(unsigned int), c->stream));
-            for (int k = 0; k < batch; ++k) {
-                for (int b = 0; b < 3; ++b) {
-                    ca.end_in[b] = cur + (size_t)b * NS;
-                    ca.end_out[b] = nxt + (size_t)b * NS;
-                }
-                ca.changed = changed + k;
-                const unsigned int *prevf = k > 0 ? changed + (k - 1) : nullptr;
-                RET(launch(c, "comp_fix", comp_fix_kernel, dim3(nbs, 3), dim3(256), 0, ca, prevf));
-                std::swap(cur, nxt);
-            }
-            unsigned int h[16];
-            HIPCHK(c, hipMemcpyAsync(h, changed, batch * sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream));
-            HIPCHK(c, hipStreamSynchronize(c->stream));
-            for (int k = 0; k < batch; ++k) {
-                if (h[k] == 0) {
-                    // sweep k changed nothing, so it copied end_in to end_out and
-                    // both buffers hold the converged ends; later sweeps exited early.
-                    done = true;
-                    break;
-                }
-                ++iters;
-            }
-            if (!done && iters >= j->comp_max_iters)
-                return set_err(c, MM_ERR_STATE, "compressor did not converge in %d sweeps", iters);
-            batch = 4;
-        }
-        c->job.comp_max_iters = iters;  // reported via mm_result
-        RET(launch(c, "comp_record", comp_record_kernel, dim3(nbs, 3), dim3(256), 0, ca));
-        RET(launch(c, "comp_tstart", comp_tstart_kernel, dim3(nb, 3), dim3(256), 0, ca));
-        RET(launch(c, "comp_apply", comp_apply_kernel, dim3(blocks_for(G, APPLY_TILES)), dim3(3 * APPLY_TILES), 0,
-                   ca));
+        c->comp_on = true;
+        c->ca = ca;
+        c->comp_cur = eA;
+        c->comp_nxt = eB;
+        c->comp_changed = changed;
+        c->comp_iters = 0;
+        c->comp_pending = 0;
+        c->comp_nb = nb;
+        c->comp_nbs = nbs;
+        RET(comp_sweeps(c, COMP_SWEEPS));
+        RET(comp_back(c));
         mix = q2;
     } else {
-        c->job.comp_max_iters = 0;
+        c->comp_on = false;
     }
     c->mix = mix;
     c->staged = true;
     return MM_OK;
 }
 
-// Synchronises the stream and reports a look-back spin timeout (never expected:
-// every block only waits on blocks that started before it).
-static int check_lb_error(mm_ctx *c) {
-    unsigned e = 0;
-    if (c->lb_error) HIPCHK(c, hipMemcpyAsync(&e, c->lb_error, 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (e) return set_err(c, MM_ERR_STATE, "IIR look-back timed out");
+// ------------------------------------------------------------ K-weighting
+// Loudness geometry on the device (segment bounds; per-block segment ranges),
+// uploaded only when the job's geometry changes.
+static int upload_geometry(mm_ctx *c) {
+    const mm_job *j = &c->job;
+    std::vector<int64_t> key;
+    key.reserve((size_t)(j->n_segs + 3 + 2 * j->n_blocks));
+    key.push_back(j->n_segs);
+    key.insert(key.end(), j->seg_bounds, j->seg_bounds + j->n_segs + 1);
+    key.push_back(j->n_blocks);
+    key.insert(key.end(), j->block_lo, j->block_lo + j->n_blocks);
+    key.insert(key.end(), j->block_hi, j->block_hi + j->n_blocks);
+    RET(get_buf(c, "kw_bounds", (size_t)j->n_segs + 1, &c->seg_bounds_dev));
+    RET(get_buf(c, "gate_s0", (size_t)j->n_blocks, &c->blk_s0));
+    RET(get_buf(c, "gate_s1", (size_t)j->n_blocks, &c->blk_s1));
+    if (key == c->geom_cache) return MM_OK;
+    std::vector<int32_t> s0((size_t)j->n_blocks), s1((size_t)j->n_blocks);
+    const int64_t *B = j->seg_bounds, S = j->n_segs;
+    for (int64_t b = 0; b < j->n_blocks; ++b) {  // as mm_gate_loudness
+        s0[b] = (int32_t)std::min<int64_t>(std::lower_bound(B, B + S + 1, j->block_lo[b]) - B, S);
+        s1[b] = (int32_t)std::min<int64_t>(std::lower_bound(B, B + S + 1, j->block_hi[b]) - B, S);
+    }
+    HIPCHK(c, hipMemcpyAsync(c->seg_bounds_dev, j->seg_bounds, (S + 1) * sizeof(int64_t), hipMemcpyHostToDevice,
+                             c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->blk_s0, s0.data(), s0.size() * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->blk_s1, s1.data(), s1.size() * 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // host vectors are transient
+    c->geom_cache = key;
     return MM_OK;
 }
 
-// ------------------------------------------------------------ K-weighting
-static int kweight_energies(mm_ctx *c, const double *carry_in_host, double *seg_host, double *range_end_host) {
+// K-weighting + per-segment energies of the staged mix (device).  Returns the
+// device segment-energy vector; `line_end` receives the state after the last
+// frame when requested.
+static int kweight_launch(mm_ctx *c, const double *carry_in_host, double *line_end, double **seg_out) {
     const mm_job *j = &c->job;
     const int64_t G = c->G;
-    double *part, *seg, *lend;
-    int64_t *part_seg, *bounds;
+    double *part, *seg;
+    int64_t *part_seg;
     RET(get_buf(c, "kw_part", (size_t)std::max<int64_t>(G, 1) * 2, &part));
     RET(get_buf(c, "kw_part_seg", (size_t)std::max<int64_t>(G, 1), &part_seg));
     RET(get_buf(c, "kw_seg", (size_t)j->n_segs, &seg));
-    RET(get_buf(c, "kw_bounds", (size_t)j->n_segs + 1, &bounds));
-    RET(get_buf(c, "kw_lend", 8, &lend));
-    HIPCHK(c, hipMemcpyAsync(bounds, j->seg_bounds, (j->n_segs + 1) * sizeof(int64_t), hipMemcpyHostToDevice,
-                             c->stream));
+    RET(upload_geometry(c));
     LbArgs lb{};
     RET(upload_tables(c, "kweight", j->kweight, lb));
     const unsigned nblk = blocks_for(G, LB_THREADS);
@@ -459,6 +526,7 @@ static int kweight_energies(mm_ctx *c, const double *carry_in_host, double *seg_
         double *init;
         RET(get_buf(c, "kw_init", 8, &init));
         HIPCHK(c, hipMemcpyAsync(init, carry_in_host, 4 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));  // pageable source
         lb.init = init;
     }
     KwArgs ka{};
@@ -470,20 +538,44 @@ static int kweight_energies(mm_ctx *c, const double *carry_in_host, double *seg_
         for (int k = 0; k < 5; ++k) ka.sos[s_][k] = j->kweight.sos[s_][k];
     ka.mix = reinterpret_cast<const int16_t *>(c->mix);
     ka.n_segs = j->n_segs;
-    ka.seg_bounds = bounds;
+    ka.seg_bounds = c->seg_bounds_dev;
     ka.part = part;
     ka.part_seg = part_seg;
-    ka.line_end = range_end_host ? lend : nullptr;
+    ka.line_end = line_end;
     RET(launch(c, "kweight", kweight_kernel, dim3(nblk), dim3(LB_THREADS), lb_lds_bytes<4, 1>(), ka, lb));
-    if (range_end_host) {
-        HIPCHK(c, hipMemcpyAsync(range_end_host, lend, 4 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-        RET(check_lb_error(c));
-        return MM_OK;
-    }
     RET(launch(c, "seg_reduce", seg_reduce_kernel, dim3(blocks_for(j->n_segs, 256)), dim3(256), 0, ka, seg));
-    HIPCHK(c, hipMemcpyAsync(seg_host, seg, j->n_segs * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-    RET(check_lb_error(c));
+    *seg_out = seg;
     return MM_OK;
+}
+
+// Host-returning variant (time-sharded ranks: carry-in state, range end state).
+static int kweight_energies(mm_ctx *c, const double *carry_in_host, double *seg_host, double *range_end_host) {
+    double *lend, *seg;
+    RET(get_buf(c, "kw_lend", 8, &lend));
+    RET(kweight_launch(c, carry_in_host, range_end_host ? lend : nullptr, &seg));
+    if (range_end_host)
+        HIPCHK(c, hipMemcpyAsync(range_end_host, lend, 4 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (seg_host)
+        HIPCHK(c, hipMemcpyAsync(seg_host, seg, c->job.n_segs * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    bool conv;
+    return chain_check(c, &conv);
+}
+
+// Whole-track loudness and gain on the device (no host round trip).
+static int kweight_device(mm_ctx *c) {
+    const mm_job *j = &c->job;
+    double *seg;
+    RET(kweight_launch(c, nullptr, nullptr, &seg));
+    RET(get_buf(c, "gate_out", 2, &c->gate_out));
+    GateArgs ga{};
+    ga.n_blocks = j->n_blocks;
+    ga.blk_s0 = c->blk_s0;
+    ga.blk_s1 = c->blk_s1;
+    ga.seg = seg;
+    ga.scale = j->block_scale;
+    ga.target = j->lufs_target;
+    ga.out = c->gate_out;
+    return launch(c, "gate", gate_kernel, dim3(1), dim3(GATE_THREADS), 0, ga);
 }
 
 // pyloudnorm 0.1.1 integrated_loudness gating (mono, G=1), restated.
@@ -522,7 +614,7 @@ extern "C" int mm_gate_loudness(const mm_job *j, const double *seg_energy, doubl
     return MM_OK;
 }
 
-static int finalize(mm_ctx *c, double gain, int use_gain, void *d_out) {
+static int finalize(mm_ctx *c, double gain, const double *gain_dev, int use_gain, void *d_out) {
     const mm_job *j = &c->job;
     if (c->G == 0) return MM_OK;
     FinArgs fa{};
@@ -533,32 +625,54 @@ static int finalize(mm_ctx *c, double gain, int use_gain, void *d_out) {
     fa.out_kind = j->out_kind;
     fa.use_gain = use_gain;
     fa.gain = gain;
+    fa.gain_dev = gain_dev;
     fa.mix = c->mix;
     fa.out = d_out;
     const size_t lds = (size_t)FIN_TILES * (j->tile + 1) * sizeof(short2);
     return launch(c, "finalize", finalize_kernel, dim3(blocks_for(c->G, FIN_TILES)), dim3(256), lds, fa);
 }
 
+// The chain is queued without host round trips; one sync at the end checks
+// the compressor's convergence (a rare unconverged batch is extended and the
+// dependent stages re-run) and fetches the loudness.
 static int master_device(mm_ctx *c, const mm_job *j, const float *d_in, void *d_out, mm_result *res) {
-    RET(stage_chunks(c, j, d_in));
-    double L = NAN, gain = 1.0;
-    int use_gain = 0;
-    if (j->lufs_on) {
-        std::vector<double> seg((size_t)j->n_segs);
-        if (c->G > 0) RET(kweight_energies(c, nullptr, seg.data(), nullptr));
-        RET(mm_gate_loudness(j, seg.data(), &L));
-        gain = std::pow(10.0, (j->lufs_target - L) / 20.0);
-        use_gain = 1;
+    RET(stage_front(c, j, d_in));
+    const bool lufs = j->lufs_on && c->G > 0;
+    for (;;) {
+        if (lufs) RET(kweight_device(c));
+        RET(finalize(c, 1.0, lufs ? c->gate_out + 1 : nullptr, j->lufs_on, d_out));
+        double lg[2] = {NAN, 1.0};
+        if (lufs) HIPCHK(c, hipMemcpyAsync(lg, c->gate_out, sizeof lg, hipMemcpyDeviceToHost, c->stream));
+        bool converged;
+        RET(chain_check(c, &converged));
+        if (converged) {
+            if (j->lufs_on && c->G == 0) {  // nothing measured: pyloudnorm would have raised earlier
+                lg[0] = -INFINITY;
+                lg[1] = INFINITY;
+            }
+            if (res) {
+                res->loudness = j->lufs_on ? lg[0] : NAN;
+                res->gain_linear = j->lufs_on ? lg[1] : 1.0;
+                res->frames_out = j->frames_proc;
+                res->comp_iters = c->comp_iters;
+            }
+            return MM_OK;
+        }
+        RET(comp_sweeps(c, 8, true));
+        RET(comp_back(c));
     }
-    RET(finalize(c, gain, use_gain, d_out));
-    if (!j->lufs_on) RET(check_lb_error(c));
-    if (res) {
-        res->loudness = L;
-        res->gain_linear = gain;
-        res->frames_out = j->frames_proc;
-        res->comp_iters = c->job.comp_max_iters;
+}
+
+// Stage the chunk chain of a range (time-sharded ranks) to convergence.
+static int stage_chunks(mm_ctx *c, const mm_job *j, const float *d_in) {
+    RET(stage_front(c, j, d_in));
+    for (;;) {
+        bool converged;
+        RET(chain_check(c, &converged));
+        if (converged) return MM_OK;
+        RET(comp_sweeps(c, 8, true));
+        RET(comp_back(c));
     }
-    return MM_OK;
 }
 
 // =================================================================== C-ABI
@@ -658,7 +772,7 @@ int mm_hop_energies(mm_ctx *c, const double *carry_in_host, double *seg_energy_h
 
 int mm_finalize(mm_ctx *c, double gain_linear, int use_gain, void *d_out) {
     if (!c || !c->staged) return set_err(c, MM_ERR_STATE, "no staged job");
-    return finalize(c, gain_linear, use_gain, d_out);
+    return finalize(c, gain_linear, nullptr, use_gain, d_out);
 }
 
 int mm_read_mix(mm_ctx *c, int16_t *host_mix) {
