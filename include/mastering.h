@@ -117,6 +117,8 @@ typedef struct mm_result {
     int64_t frames_out;      /* == frames_proc                                   */
     int32_t comp_iters;      /* fix-up sweeps the compressor needed              */
     int32_t _pad;
+    int64_t comp_active;     /* active (M != 0) frames over the three bands      */
+    int64_t comp_walked;     /* frames re-walked by the fix-up sweeps            */
 } mm_result;
 
 /* ---- context ------------------------------------------------------------ */

@@ -131,6 +131,7 @@ struct CompArgs {
     const double *end_in[3];
     double *end_out[3];
     unsigned int *changed;
+    unsigned long long *walked;  // frames re-walked by the fix-up sweeps (statistics)
     short2 *q_out;
 };
 

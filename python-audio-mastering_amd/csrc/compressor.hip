@@ -322,6 +322,7 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
     if (need) {
         a.start[b][s] = want;
         *a.changed = 1u;  // benign race: every writer stores 1
+        atomicAdd(a.walked, (unsigned long long)st.len);
     }
     if (live) a.end_out[b][s] = e;
 }

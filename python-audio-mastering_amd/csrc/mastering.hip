@@ -271,7 +271,7 @@ static int comp_sweeps(mm_ctx *c, int n, bool resume = false) {
     // comp_record overwrote Mc with attenuations: restore M before resuming
     if (resume) RET(launch(c, "comp_compact", comp_compact_kernel, dim3(c->comp_nb, 3), dim3(256), 0, ca));
     const int64_t NS = ca.GS;
-    HIPCHK(c, hipMemsetAsync(c->comp_changed, 0, 16 * sizeof(unsigned int), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->comp_changed, 0, 16 * sizeof(unsigned int), c->stream));  // flags only
     for (int k = 0; k < n; ++k) {
         for (int b = 0; b < 3; ++b) {
             ca.end_in[b] = c->comp_cur + (size_t)b * NS;
@@ -413,6 +413,8 @@ static int stage_front(mm_ctx *c, const mm_job *j, const float *d_in) {
         RET(get_buf(c, "comp_lut", (size_t)3 * 32769, &luts));
         unsigned int *changed;
         RET(get_buf(c, "comp_changed", 64, &changed));
+        ca.walked = reinterpret_cast<unsigned long long *>(changed + 32);
+        HIPCHK(c, hipMemsetAsync(ca.walked, 0, 8, c->stream));
         int32_t *cnt, *off, *tot;
         RET(get_buf(c, "comp_cnt", (size_t)3 * G, &cnt));
         RET(get_buf(c, "comp_off", (size_t)3 * G, &off));
@@ -643,6 +645,15 @@ static int master_device(mm_ctx *c, const mm_job *j, const float *d_in, void *d_
         RET(finalize(c, 1.0, lufs ? c->gate_out + 1 : nullptr, j->lufs_on, d_out));
         double lg[2] = {NAN, 1.0};
         if (lufs) HIPCHK(c, hipMemcpyAsync(lg, c->gate_out, sizeof lg, hipMemcpyDeviceToHost, c->stream));
+        unsigned long long walked = 0;
+        std::vector<int32_t> totals;
+        if (res && c->comp_on) {
+            const int64_t nchunks = c->ca.GS / c->ca.SPC;
+            totals.resize((size_t)3 * nchunks);
+            HIPCHK(c, hipMemcpyAsync(totals.data(), c->ca.total[0], totals.size() * 4, hipMemcpyDeviceToHost,
+                                     c->stream));
+            HIPCHK(c, hipMemcpyAsync(&walked, c->ca.walked, 8, hipMemcpyDeviceToHost, c->stream));
+        }
         bool converged;
         RET(chain_check(c, &converged));
         if (converged) {
@@ -655,6 +666,9 @@ static int master_device(mm_ctx *c, const mm_job *j, const float *d_in, void *d_
                 res->gain_linear = j->lufs_on ? lg[1] : 1.0;
                 res->frames_out = j->frames_proc;
                 res->comp_iters = c->comp_iters;
+                res->comp_active = 0;
+                for (int32_t t : totals) res->comp_active += t;
+                res->comp_walked = (int64_t)walked;
             }
             return MM_OK;
         }

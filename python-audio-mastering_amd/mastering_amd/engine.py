@@ -178,11 +178,12 @@ def master_pcm(pcm: np.ndarray, rate: int, params: dict, out_kind: int = native.
     return out, info
 
 
-def master_device(ctx: native.Context, job: Job, d_in: int, d_out: int):
-    """Device-resident variant (pointers from e.g. torch tensors)."""
-    res = native.MMResult()
+def master_device(ctx: native.Context, job: Job, d_in: int, d_out: int, res: native.MMResult | None = None):
+    """Device-resident variant (pointers from e.g. torch tensors).  With `res`
+    the loudness, gain and compressor statistics are returned in it."""
     ctx.check(ctx.lib.mm_master_device(ctx.ptr, ctypes.byref(job.job), ctypes.c_void_p(d_in),
-                                       ctypes.c_void_p(d_out), ctypes.byref(res)), "mm_master_device")
+                                       ctypes.c_void_p(d_out), ctypes.byref(res) if res is not None else None),
+              "mm_master_device")
     return res
 
 

@@ -49,7 +49,8 @@ class MMJob(ctypes.Structure):
 
 class MMResult(ctypes.Structure):
     _fields_ = [("loudness", ctypes.c_double), ("gain_linear", ctypes.c_double), ("frames_out", ctypes.c_int64),
-                ("comp_iters", ctypes.c_int32), ("_pad", ctypes.c_int32)]
+                ("comp_iters", ctypes.c_int32), ("_pad", ctypes.c_int32),
+                ("comp_active", ctypes.c_int64), ("comp_walked", ctypes.c_int64)]
 
 
 # every symbol include/mastering.h declares (checked by tests/test_abi.py)
