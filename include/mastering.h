@@ -98,7 +98,7 @@ typedef struct mm_job {
     mm_iir xover;            /* butter(4) LP250 (branch 0) + HP4000 (branch 1)  */
     mm_iir kweight;          /* pyloudnorm high_shelf then high_pass            */
     mm_band band[3];         /* low / mid / high                                */
-    int32_t comp_warmup;     /* >0: speculative warm-up over the previous super-tile */
+    int32_t comp_warmup;     /* super-tiles of speculative warm-up walk before each one */
     int32_t comp_max_iters;  /* cap on fix-up sweeps (exactness check)          */
     int32_t comp_super;      /* frames per super-tile of the envelope solve (rounded to whole tiles) */
     int32_t _pad2;

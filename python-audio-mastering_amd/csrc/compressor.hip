@@ -246,7 +246,10 @@ __device__ __forceinline__ double comp_walk(double att, const CompArgs &a, int b
     return att;
 }
 
-// 4. speculative pass.  grid: (ceil(GS/256), 3)
+// 4. speculative pass.  grid: (ceil(GS/256), 3).  The start of super-tile s
+// is guessed by walking the `warmup` previous super-tiles of its chunk, from the
+// M of the first warm-up frame (the state tracks M closely: this coalesces with
+// the true trajectory far more often than a start at 0; tools/ studies).
 __global__ void __launch_bounds__(256) comp_pass0_kernel(CompArgs a) {
     const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int b = blockIdx.y;
@@ -255,30 +258,37 @@ __global__ void __launch_bounds__(256) comp_pass0_kernel(CompArgs a) {
     if (st.len == 0) return;
     const BandStep bs = band_step(a, b);
     double att = 0.0;
-    if (a.warmup > 0 && st.p0 > 0) att = comp_walk<false>(att, a, b, s - 1, a.U, bs);
+    if (a.warmup > 0 && st.p0 > 0) {
+        const int64_t k = st.p0 / a.U;  // index of s within its chunk
+        const int64_t w0 = s - min((int64_t)a.warmup, k);
+        att = a.Mc[b][w0];  // row 0 of super-tile w0
+        for (int64_t w = w0; w < s; ++w) att = comp_walk<false>(att, a, b, w, a.U, bs);
+    }
     a.start[b][s] = att;
     a.end_out[b][s] = comp_walk<false>(att, a, b, s, st.len, bs);
 }
 
 // 5. one Jacobi sweep (exits at once if the previous sweep changed nothing).
-// grid: (ceil(GS/64), 3), one wave per block.  A lane whose start changed
-// re-walks its super-tile.  When only a few lanes of the wave walk (the later
-// sweeps, where only the chains of non-coalescing super-tiles remain), the whole
-// wave serves them one at a time: it loads the super-tile's M values and
-// computes M/A and M/R in parallel into LDS, then the walking lane runs the lean
-// step from LDS (~50 instead of ~130 cycles per step for a lone lane that also
-// divides; tools/micro/step_bench.hip).
-constexpr int FIX_COOP_MAX = 4;     // walkers per wave served cooperatively
-constexpr int FIX_MAX_U = 1024;     // LDS capacity (frames per super-tile)
+// grid: (ceil(GS/64), 3), one wave per block, lane = super-tile.  A lane whose
+// start changed re-walks its super-tile.  When at most FIX_SLOTS lanes of the
+// wave walk (every sweep once the warm-up guesses are good), the wave serves
+// them together: chunk by chunk, all 64 lanes load the walkers' next M values
+// (prefetched one chunk ahead) and compute M/A and M/R into LDS, then every
+// walker runs the lean step (add, min, select: ~50 cycles instead of ~130 for a
+// lone lane that also divides; tools/micro/step_bench.hip) from LDS.
+constexpr int FIX_SLOTS = 16;   // walkers per wave served from LDS
+constexpr int FIX_CHUNK = 64;   // frames per walker per staging round
+constexpr int FIX_MAX_U = 8192; // cap on frames per super-tile (slot lengths are int)
 
 __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned int *prev_changed) {
-    __shared__ double sm[FIX_MAX_U], si[FIX_MAX_U], sd[FIX_MAX_U];
+    __shared__ double sm[FIX_SLOTS][FIX_CHUNK + 1], si[FIX_SLOTS][FIX_CHUNK + 1], sd[FIX_SLOTS][FIX_CHUNK + 1];
+    __shared__ int slot_lane[FIX_SLOTS], slot_len[FIX_SLOTS];
     if (prev_changed && *prev_changed == 0u) return;
     const int lane = threadIdx.x;
     const int64_t s = (int64_t)blockIdx.x * 64 + lane;
     const int b = blockIdx.y;
     const bool valid = s < a.GS;
-    const Super st = valid ? super_of(a, b, s) : Super{0, 0, 0};
+    const Super st = valid ? super_of(a, b, s) : Super{0, 0, 0, false};
     const bool live = valid && st.len > 0;
     const double *end_in = a.end_in[b];
     double e = live ? end_in[s] : 0.0;
@@ -289,35 +299,58 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
         need = __double_as_longlong(want) != __double_as_longlong(a.start[b][s]);
     }
     const BandStep bs = band_step(a, b);
-    unsigned long long m = __ballot(need);
-    if (__popcll(m) > FIX_COOP_MAX) {
+    const unsigned long long m = __ballot(need);
+    const int k = __popcll(m);
+    if (k > FIX_SLOTS) {
         if (need) e = comp_walk<false>(want, a, b, s, st.len, bs);
-    } else {
+    } else if (k > 0) {
+        const int slot = __popcll(m & ((1ull << lane) - 1));
+        if (need) {
+            slot_lane[slot] = lane;
+            slot_len[slot] = st.len;
+        }
+        __syncthreads();
+        int maxlen = 0;
+        for (int w = 0; w < k; ++w) maxlen = max(maxlen, slot_len[w]);
         const double *Mc = a.Mc[b];
-        while (m) {  // wave-uniform
-            const int j = __builtin_ctzll(m);
-            m &= m - 1;
-            const int len = __shfl(st.len, j);
-            const int64_t sj = (int64_t)blockIdx.x * 64 + j;
-            for (int i = lane; i < len; i += 64) {
-                const double mv = Mc[(int64_t)i * a.GS + sj];
-                sm[i] = mv;
-                si[i] = div_cr(mv, bs.A, bs.rA);
-                sd[i] = div_cr(mv, bs.R, bs.rR);
+        const int64_t col0 = (int64_t)blockIdx.x * 64;
+        double pre[FIX_SLOTS];  // lane = frame offset in the chunk, r = walker slot
+        auto load_chunk = [&](int base) {
+#pragma unroll
+            for (int r = 0; r < FIX_SLOTS; ++r) {
+                if (r < k) {
+                    const int i = base + lane;
+                    pre[r] = i < slot_len[r] ? Mc[(int64_t)i * a.GS + col0 + slot_lane[r]] : 0.0;
+                }
+            }
+        };
+        load_chunk(0);
+        double att = want;
+        for (int base = 0; base < maxlen; base += FIX_CHUNK) {
+#pragma unroll
+            for (int r = 0; r < FIX_SLOTS; ++r) {
+                if (r < k) {
+                    const double mv = pre[r];
+                    sm[r][lane] = mv;
+                    si[r][lane] = div_cr(mv, bs.A, bs.rA);
+                    sd[r][lane] = div_cr(mv, bs.R, bs.rR);
+                }
             }
             __syncthreads();
-            if (lane == j) {
-                double att = want;
+            if (base + FIX_CHUNK < maxlen) load_chunk(base + FIX_CHUNK);
+            if (need) {
+                const int lim = min(FIX_CHUNK, st.len - base);
+                const double *pm = sm[slot], *pi = si[slot], *pd = sd[slot];
 #pragma unroll 8
-                for (int i = 0; i < len; ++i) {
-                    const double up = fmin(att + si[i], sm[i]);
-                    const double dn = fmax(att - sd[i], 0.0);
-                    att = att <= sm[i] ? up : dn;
+                for (int f = 0; f < lim; ++f) {
+                    const double up = fmin(att + pi[f], pm[f]);
+                    const double dn = fmax(att - pd[f], 0.0);
+                    att = att <= pm[f] ? up : dn;
                 }
-                e = att;
             }
             __syncthreads();
         }
+        if (need) e = att;
     }
     if (need) {
         a.start[b][s] = want;
