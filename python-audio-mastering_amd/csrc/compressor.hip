@@ -37,23 +37,28 @@
 
 namespace mm {
 
-__device__ __forceinline__ int32_t frame_energy(short2 v) {
-    return (int32_t)v.x * v.x + (int32_t)v.y * v.y;
+// x^2 + y^2 of one frame: at most 2 * 32768^2 = 2^31, exact in uint32
+__device__ __forceinline__ uint32_t frame_energy(short2 v) {
+    return (uint32_t)((int32_t)v.x * v.x) + (uint32_t)((int32_t)v.y * v.y);
 }
 
-// largest r with n*r*r <= S (== trunc(sqrt(S/n)) computed in doubles)
-__device__ __forceinline__ uint32_t rms_exact(int64_t S, int64_t n, float inv_n) {
-    int64_t r = (int64_t)__fsqrt_rn((float)S * inv_n);
-    r -= (r > 0 && n * r * r > S);
-    r += (n * (r + 1) * (r + 1) <= S);
-    return n > 0 ? (uint32_t)r : 0u;
+// largest r with n*r*r <= S (== isqrt(S div n) == trunc(sqrt(S/n)) computed in
+// doubles, tests/test_oracle.py).  S and n*r*r are integers below 2^53, so the
+// f64 products and compares are exact; the f32 estimate is within 1 of r.
+__device__ __forceinline__ uint32_t rms_exact(double S, double n, float inv_n) {
+    int32_t r = (int32_t)__fsqrt_rn((float)S * inv_n);
+    double rd = (double)r;
+    r -= (n * rd * rd > S) ? 1 : 0;
+    rd = (double)(r + 1);
+    r += (n * rd * rd <= S) ? 1 : 0;
+    return n > 0.0 ? (uint32_t)r : 0u;
 }
 
 // 1. rms per frame (uint16 r, tile-major).  grid: (ceil(G/256), 3 bands).  The
 // window [max(chunk0, f-look), f) slides one frame per step: + frame f-1 (this
 // lane's own previous frame), - frame f-1-look (up to ~4 tiles back: another
-// lane's data, coalesced across the wave).  Frame -> (tile, offset) arithmetic is
-// incremental: no 64-bit division per frame.
+// lane's data, coalesced across the wave).  The window sum is an exact integer
+// held in a double; element indices fit 32 bits (frames < 2^31).
 __global__ void __launch_bounds__(256) comp_rms_kernel(CompArgs a) {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int b = blockIdx.y;
@@ -61,28 +66,30 @@ __global__ void __launch_bounds__(256) comp_rms_kernel(CompArgs a) {
     const short2 *x = a.band[b];
     const int look = a.look[b];
     const int T = a.T;
-    const int64_t G = a.G;
+    const uint32_t G = (uint32_t)a.G, g32 = (uint32_t)g;
     const int64_t f0 = g * T;
     const int64_t chunk0 = (g / a.K) * a.K * T;
     const int len = (int)min((int64_t)T, a.N_proc - f0);
-    const int ch = a.ch;
     // warm-up: S over [lo0, f0)
     const int64_t lo0 = max(chunk0, f0 - look);
-    const int64_t gw = lo0 / T;
-    const int nw = (int)(lo0 - gw * T);
-    int64_t S = 0;
-    for (int64_t gt = gw, n_first = nw; gt < g; ++gt, n_first = 0) {  // <= look/T + 1 tiles
-#pragma unroll 8
-        for (int n = (int)n_first; n < T; ++n) S += frame_energy(x[(int64_t)n * G + gt]);
+    const uint32_t gw = (uint32_t)(lo0 / T);
+    double S = 0.0;
+    {
+        uint32_t gt = gw, n = (uint32_t)(lo0 - (int64_t)gw * T);
+        for (; gt < g32; ++gt, n = 0) {  // <= look/T + 1 tiles
+#pragma unroll 5
+            for (; n < (uint32_t)T; ++n) S += (double)frame_energy(x[n * G + gt]);
+        }
     }
     // drop frames: d = f - look for f >= chunk0 + look; the first `skip` frames drop nothing
     const int64_t d_first = max(f0 - look, chunk0);
     const int skip = (int)(d_first - (f0 - look));
-    const int64_t gd = d_first / T;
-    const int nd = (int)(d_first - gd * T);
+    const uint32_t gd = (uint32_t)(d_first / T);
+    const int nd = (int)(d_first - (int64_t)gd * T);
     uint16_t *R = a.r16[b];
-    int64_t cnt = f0 - lo0;
-    float inv = cnt > 0 ? 1.0f / (float)(cnt * ch) : 0.f;
+    const int ch = a.ch;
+    double n = (double)((f0 - lo0) * ch);
+    float inv = n > 0.0 ? 1.0f / (float)n : 0.f;
     const uint32_t r0 = a.r0[b];
     int i_proc = 0, active = 0;
     struct Pair {
@@ -93,23 +100,22 @@ __global__ void __launch_bounds__(256) comp_rms_kernel(CompArgs a) {
         [&](int i) {
             i = min(i, len - 1);
             Pair p;
-            p.in = x[(int64_t)i * G + g];
+            p.in = x[(uint32_t)i * G + g32];
             int k = nd + max(i - skip, 0);  // < 2T
-            const int wrap = k >= T;
-            k -= wrap ? T : 0;
-            p.drop = x[(int64_t)k * G + gd + wrap];
+            const int wrap = k >= T ? 1 : 0;
+            k -= wrap * T;
+            p.drop = x[(uint32_t)k * G + gd + (uint32_t)wrap];
             return p;
         },
         [&](Pair p) {
-            const uint32_t r = rms_exact(S, cnt * ch, inv);
-            R[(int64_t)i_proc * G + g] = (uint16_t)r;
-            active += r >= r0;
-            S += frame_energy(p.in);
-            if (i_proc >= skip) {
-                S -= frame_energy(p.drop);
-            } else {
-                ++cnt;
-                inv = 1.0f / (float)(cnt * ch);
+            const uint32_t r = rms_exact(S, n, inv);
+            R[(uint32_t)i_proc * G + g32] = (uint16_t)r;
+            active += r >= r0 ? 1 : 0;
+            const bool drops = i_proc >= skip;
+            S += (double)frame_energy(p.in) - (drops ? (double)frame_energy(p.drop) : 0.0);
+            if (!drops) {  // window still growing (first `look` frames of a chunk only)
+                n += ch;
+                inv = 1.0f / (float)n;
             }
             ++i_proc;
         });

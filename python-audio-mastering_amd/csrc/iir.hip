@@ -68,6 +68,10 @@ template <int CH>
 constexpr int eq_stage_bytes() {
     return 2 * (LB_THREADS / CH) * (EQ_STAGE + 1) * CH * (int)sizeof(float);
 }
+template <int NS, int CH>
+constexpr int eq_lds_bytes() {
+    return eq_stage_bytes<CH>() > lb_lds_bytes<2 * NS, CH>() ? eq_stage_bytes<CH>() : lb_lds_bytes<2 * NS, CH>();
+}
 
 // One pass over the block's tiles with the input staged through LDS: the block
 // cooperatively loads EQ_STAGE frames of each of its tiles (16 consecutive
@@ -161,8 +165,10 @@ __global__ void __launch_bounds__(LB_THREADS, 4) eq_kernel(EqArgs a, LbArgs lb, 
     const int64_t g = g0 + t;
     const bool valid = g < a.G;
     const int len = valid ? (int)min((int64_t)a.T, a.N_proc - g * a.T) : 0;
+    // the look-back scratch is live only between the passes: it aliases the
+    // staging buffer, so four blocks fit a CU (eq_lds_bytes)
     float *stage = reinterpret_cast<float *>(smem);
-    double *lds = smem + eq_stage_bytes<CH>() / 8;
+    double *lds = smem;
     double zs[NS][2];
 #pragma unroll
     for (int s = 0; s < NS; ++s) zs[s][0] = zs[s][1] = 0.0;
@@ -176,6 +182,7 @@ __global__ void __launch_bounds__(LB_THREADS, 4) eq_kernel(EqArgs a, LbArgs lb, 
 #pragma unroll
     for (int d = 0; d < DIM; ++d) rst[d] = 0.0;
     lb_carry<DIM, CH>(lb, blk, t, c, valid, valid && (g % line_tiles) == 0, rst, z, s, lds);
+    __syncthreads();  // every lane has read the look-back scratch before pass 2 stages into it
 #pragma unroll
     for (int s_ = 0; s_ < NS; ++s_) {
         zs[s_][0] = s[2 * s_];
@@ -366,21 +373,25 @@ __global__ void __launch_bounds__(LB_THREADS, 2) kweight_kernel(KwArgs a, LbArgs
     }
 }
 
-// Sum the per-tile partials into loudness segments (deterministic order).
-__global__ void seg_reduce_kernel(KwArgs a, double *seg_energy) {
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= a.n_segs) return;
+// Sum the per-tile partials into loudness segments: one wave per segment, lane
+// k takes tiles g0+k, g0+k+64, ...; fixed-order butterfly (deterministic).
+__global__ void __launch_bounds__(256) seg_reduce_kernel(KwArgs a, double *seg_energy) {
+    const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (s >= a.n_segs) return;  // wave-uniform
     int64_t b0 = a.seg_bounds[s], b1 = a.seg_bounds[s + 1];
     if (b1 > a.N_proc) b1 = a.N_proc;
     double acc = 0.0;
     if (b0 < b1) {
         const int64_t g0 = b0 / a.T, g1 = (b1 - 1) / a.T;
-        for (int64_t g = g0; g <= g1; ++g) {
-            if (a.part_seg[g] == s) acc += a.part[2 * g];
-            else if (a.part_seg[g] == s - 1) acc += a.part[2 * g + 1];
+        for (int64_t g = g0 + lane; g <= g1; g += 64) {
+            const int64_t ps = a.part_seg[g];
+            acc += ps == s ? a.part[2 * g] : (ps == s - 1 ? a.part[2 * g + 1] : 0.0);
         }
     }
-    seg_energy[s] = acc;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off);
+    if (lane == 0) seg_energy[s] = acc;
 }
 
 }  // namespace mm

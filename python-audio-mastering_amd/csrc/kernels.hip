@@ -52,6 +52,7 @@ __device__ __forceinline__ float limiter32(float y) {
     return y;
 }
 
+template <int CH>
 __global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
     extern __shared__ short2 lds[];  // [FIN_TILES][T+1]
     const int T = a.T;
@@ -59,36 +60,41 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
     const int64_t g0 = (int64_t)blockIdx.x * FIN_TILES;
     const int ntile = (int)min((int64_t)FIN_TILES, a.G - g0);
     for (int i = threadIdx.x; i < T * FIN_TILES; i += blockDim.x) {
-        int n = i / FIN_TILES, t = i - n * FIN_TILES;
+        const int n = i / FIN_TILES, t = i % FIN_TILES;
         if (t < ntile) lds[t * stride + n] = a.mix[(int64_t)n * a.G + g0 + t];
     }
     __syncthreads();
     const int64_t f_base = g0 * T;
-    const int64_t nf = min((int64_t)ntile * T, a.N_proc - f_base);
+    const int nf = (int)min((int64_t)ntile * T, a.N_proc - f_base);
     const double gain = a.gain_dev ? *a.gain_dev : a.gain;
-    for (int64_t i = threadIdx.x; i < nf; i += blockDim.x) {
-        int t = (int)(i / T), n = (int)(i - (int64_t)t * T);
-        short2 q = lds[t * stride + n];
-        int16_t o[2];
+    // frame i of the block = (tile t, offset n); t, n advance incrementally
+    // (no division per frame: the stride 256 is below T * FIN_TILES)
+    int t = (int)((unsigned)threadIdx.x / (unsigned)T), n = (int)threadIdx.x - t * T;
+    const int dt = 256 / T, dn = 256 - dt * T;
+    for (int i = threadIdx.x; i < nf; i += 256) {
+        const short2 q = lds[t * stride + n];
         const int16_t qq[2] = {q.x, q.y};
-        for (int c = 0; c < a.ch; ++c) {
-            float y = (float)qq[c] / 32768.0f;
-            if (a.use_gain) {
-                double v = (double)y * gain;
-                o[c] = quantize(limiter64(v));
-            } else {
-                o[c] = quantize((double)limiter32(y));
-            }
+        int16_t o[2];
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            const float y = (float)qq[c] / 32768.0f;
+            o[c] = a.use_gain ? quantize(limiter64((double)y * gain)) : quantize((double)limiter32(y));
         }
         const int64_t f = f_base + i;
         if (a.out_kind == 0) {
             int16_t *out = reinterpret_cast<int16_t *>(a.out);
-            if (a.ch == 2) *reinterpret_cast<short2 *>(out + 2 * f) = make_short2(o[0], o[1]);
+            if (CH == 2) *reinterpret_cast<short2 *>(out + 2 * f) = make_short2(o[0], o[1]);
             else out[f] = o[0];
         } else {
             float *out = reinterpret_cast<float *>(a.out);
-            if (a.ch == 2) *reinterpret_cast<float2 *>(out + 2 * f) = make_float2(o[0] / 32768.0f, o[1] / 32768.0f);
-            else out[f] = o[0] / 32768.0f;
+            if (CH == 2) *reinterpret_cast<float2 *>(out + 2 * f) = make_float2(o[0] * (1.0f / 32768.0f), o[1] * (1.0f / 32768.0f));
+            else out[f] = o[0] * (1.0f / 32768.0f);
+        }
+        t += dt;
+        n += dn;
+        if (n >= T) {
+            n -= T;
+            ++t;
         }
     }
 }

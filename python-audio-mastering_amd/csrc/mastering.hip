@@ -208,6 +208,8 @@ static int validate(mm_ctx *c, const mm_job *j) {
     if (j->tile < 16 || j->tile > 4096) return set_err(c, MM_ERR_ARG, "tile %d out of range", j->tile);
     if (j->tiles_per_chunk < 1) return set_err(c, MM_ERR_ARG, "tiles_per_chunk < 1");
     if (j->frames_proc < 0 || j->frames_in < 0) return set_err(c, MM_ERR_ARG, "negative frame count");
+    if (j->frames_proc >= (int64_t)1 << 31 || j->frames_in >= (int64_t)1 << 31)
+        return set_err(c, MM_ERR_ARG, "track longer than 2^31 frames (32-bit frame indexing)");
     if (j->eq.nsec < 0 || j->eq.nsec > 4) return set_err(c, MM_ERR_ARG, "eq.nsec %d", j->eq.nsec);
     const int tpb = LB_THREADS / j->channels;
     if (j->eq.nsec > 0 && j->eq.tpb != tpb) return set_err(c, MM_ERR_ARG, "eq tables built for %d tiles/block, need %d", j->eq.tpb, tpb);
@@ -243,10 +245,10 @@ static void fill_sos(double dst[4][5], const mm_iir &f, int n) {
 template <int NS>
 static int launch_eq_ns(mm_ctx *c, int ch, unsigned nblk, const EqArgs &ea, const LbArgs &lb, int64_t K) {
     if (ch == 2) {
-        const size_t lds = eq_stage_bytes<2>() + lb_lds_bytes<2 * NS, 2>();
+        const size_t lds = eq_lds_bytes<NS, 2>();
         return launch(c, "eq", eq_kernel<NS, 2>, dim3(nblk), dim3(LB_THREADS), lds, ea, lb, K);
     }
-    const size_t lds = eq_stage_bytes<1>() + lb_lds_bytes<2 * NS, 1>();
+    const size_t lds = eq_lds_bytes<NS, 1>();
     return launch(c, "eq", eq_kernel<NS, 1>, dim3(nblk), dim3(LB_THREADS), lds, ea, lb, K);
 }
 
@@ -545,7 +547,7 @@ static int kweight_launch(mm_ctx *c, const double *carry_in_host, double *line_e
     ka.part_seg = part_seg;
     ka.line_end = line_end;
     RET(launch(c, "kweight", kweight_kernel, dim3(nblk), dim3(LB_THREADS), lb_lds_bytes<4, 1>(), ka, lb));
-    RET(launch(c, "seg_reduce", seg_reduce_kernel, dim3(blocks_for(j->n_segs, 256)), dim3(256), 0, ka, seg));
+    RET(launch(c, "seg_reduce", seg_reduce_kernel, dim3(blocks_for(j->n_segs, 4)), dim3(256), 0, ka, seg));  // wave per segment
     *seg_out = seg;
     return MM_OK;
 }
@@ -631,7 +633,9 @@ static int finalize(mm_ctx *c, double gain, const double *gain_dev, int use_gain
     fa.mix = c->mix;
     fa.out = d_out;
     const size_t lds = (size_t)FIN_TILES * (j->tile + 1) * sizeof(short2);
-    return launch(c, "finalize", finalize_kernel, dim3(blocks_for(c->G, FIN_TILES)), dim3(256), lds, fa);
+    if (fa.ch == 2)
+        return launch(c, "finalize", finalize_kernel<2>, dim3(blocks_for(c->G, FIN_TILES)), dim3(256), lds, fa);
+    return launch(c, "finalize", finalize_kernel<1>, dim3(blocks_for(c->G, FIN_TILES)), dim3(256), lds, fa);
 }
 
 // The chain is queued without host round trips; one sync at the end checks

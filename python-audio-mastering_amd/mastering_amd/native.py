@@ -11,7 +11,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmastering_amd.so")
+# MM_LIB: an alternative build of the same library (tools/ablation experiments only)
+LIB_PATH = os.environ.get("MM_LIB") or os.path.join(_HERE, "libmastering_amd.so")
 
 MM_OUT_I16, MM_OUT_F32 = 0, 1
 MAX_DIM, TILE_POW, BLK_POW = 8, 8, 65
