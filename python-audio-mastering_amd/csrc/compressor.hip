@@ -235,20 +235,85 @@ __device__ __forceinline__ Super super_of(const CompArgs &a, int b, int64_t s) {
     return r;
 }
 
-// Walk the envelope over a super-tile's compacted frames (branch-free
-// software-pipelined stream).  With STORE, overwrite each compacted M with the
-// att after that frame.
+// v_min_f64 / v_max_f64 without the operand canonicalisation fmin/fmax add
+// (operands here are never NaN; equal operands and signed zeros give the same
+// observable att)
+__device__ __forceinline__ double vmin(double x, double y) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+    return r;
+}
+__device__ __forceinline__ double vmax0(double x) {
+    double r;
+    asm("v_max_f64 %0, %1, 0" : "=v"(r) : "v"(x));
+    return r;
+}
+
+// the step given M and its (precomputed) increments
+__device__ __forceinline__ double lean_step(double att, double m, double inc, double dec) {
+    const double up = vmin(att + inc, m);
+    const double dn = vmax0(att - dec);
+    return att <= m ? up : dn;
+}
+
+// Walk the envelope over a super-tile's compacted frames.  M streams WB frames
+// ahead in registers; the two divisions run WP frames ahead of the step that
+// uses them, so they issue while the att chain of earlier frames is in flight
+// (in-order issue: tools/micro/walk2_bench.hip, 136 -> 98 cycles per step).
+// With STORE, overwrite each compacted M with the att after that frame.
 template <bool STORE>
 __device__ __forceinline__ double comp_walk(double att, const CompArgs &a, int b, int64_t s, int len,
                                             const BandStep &bs) {
-    double *Mc = a.Mc[b];
-    int o = 0;
+    constexpr int WB = 32, WP = 4;
+    if (len <= 0) return att;
+    double *col = a.Mc[b] + s;  // column s, rows GS apart (compacted frames < 2^31 / GS rows)
+    const uint32_t GS = (uint32_t)a.GS;
+    const int last = len - 1;
+    double buf[WB], inc[WP], dec[WP];
+#pragma unroll
+    for (int k = 0; k < WB; ++k) buf[k] = col[(uint32_t)min(k, last) * GS];
+#pragma unroll
+    for (int k = 0; k < WP; ++k) {
+        inc[k] = div_cr(buf[k], bs.A, bs.rA);
+        dec[k] = div_cr(buf[k], bs.R, bs.rR);
+    }
+    int i = 0;
+    for (; i + WB <= len; i += WB) {
+#pragma unroll
+        for (int k = 0; k < WB; ++k) {
+            const double m = buf[k], ik = inc[k % WP], dk = dec[k % WP];
+            const double mn = buf[(k + WP) % WB];  // frame i+k+WP (already reloaded when k+WP >= WB)
+            inc[k % WP] = div_cr(mn, bs.A, bs.rA);
+            dec[k % WP] = div_cr(mn, bs.R, bs.rR);
+            att = lean_step(att, m, ik, dk);
+            if (STORE) col[(uint32_t)(i + k) * GS] = att;
+            buf[k] = col[(uint32_t)min(i + WB + k, last) * GS];
+        }
+    }
+    const int rem = len - i;
+#pragma unroll
+    for (int k = 0; k < WB; ++k) {
+        if (k < rem) {
+            const double m = buf[k], ik = inc[k % WP], dk = dec[k % WP];
+            const double mn = buf[(k + WP) % WB];
+            inc[k % WP] = div_cr(mn, bs.A, bs.rA);
+            dec[k % WP] = div_cr(mn, bs.R, bs.rR);
+            att = lean_step(att, m, ik, dk);
+            if (STORE) col[(uint32_t)(i + k) * GS] = att;
+        }
+    }
+    return att;
+}
+
+// Compact streamed walk (no STORE) for the fix kernel's lane path, where the
+// register budget is shared with the LDS-staged path.
+__device__ __forceinline__ double comp_walk_lean(double att, const CompArgs &a, int b, int64_t s, int len,
+                                                 const BandStep &bs) {
+    const double *col = a.Mc[b] + s;
+    const uint32_t GS = (uint32_t)a.GS;
     stream<8, 4, double>(
-        len, [&](int i) { return Mc[(int64_t)min(i, len - 1) * a.GS + s]; },
-        [&](double m) {
-            att = comp_step(att, m, bs);
-            if (STORE) Mc[(int64_t)(o++) * a.GS + s] = att;
-        });
+        len, [&](int i) { return col[(uint32_t)min(i, len - 1) * GS]; },
+        [&](double m) { att = comp_step(att, m, bs); });
     return att;
 }
 
@@ -308,7 +373,7 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
     const unsigned long long m = __ballot(need);
     const int k = __popcll(m);
     if (k > FIX_SLOTS) {
-        if (need) e = comp_walk<false>(want, a, b, s, st.len, bs);
+        if (need) e = comp_walk_lean(want, a, b, s, st.len, bs);
     } else if (k > 0) {
         const int slot = __popcll(m & ((1ull << lane) - 1));
         if (need) {

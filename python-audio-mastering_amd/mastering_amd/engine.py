@@ -29,7 +29,7 @@ EQ_PRESETS = {
              "description": "Warm low-mids for guitars and punchy presence for snare/vocals."},
 }
 
-COMP_WARMUP = int(os.environ.get("MM_COMP_WARMUP", "4"))  # super-tiles of warm-up walk before each one
+COMP_WARMUP = int(os.environ.get("MM_COMP_WARMUP", "6"))  # super-tiles of warm-up walk before each one
 COMP_MAX_ITERS = 100000
 # envelope solve unit (active frames) -> ~8 Jacobi sweeps on pink noise; MM_COMP_SUPER overrides
 COMP_SUPER_FRAMES = int(os.environ.get("MM_COMP_SUPER", "1000"))
