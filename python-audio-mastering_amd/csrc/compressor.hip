@@ -152,34 +152,36 @@ __global__ void __launch_bounds__(1024) comp_offsets_kernel(CompArgs a) {
 }
 
 // 3. scatter M of active frames into the compacted array.  grid (ceil(G/256), 3)
+// Inactive frames store into this lane's own padding slot (row U of the array),
+// so every store is unconditional; the element index is 32-bit and advanced
+// with selects (no per-frame branch), keeping the load pipeline counted.
 __global__ void __launch_bounds__(256) comp_compact_kernel(CompArgs a) {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int b = blockIdx.y;
     if (g >= a.G) return;
     if (a.cnt[b][g] == 0) return;
-    const uint16_t *R = a.r16[b];
+    const uint32_t G32 = (uint32_t)a.G, g32 = (uint32_t)g, GS = (uint32_t)a.GS, U = (uint32_t)a.U;
+    const uint16_t *R = a.r16[b] + g32;
     const double *lut = a.lut[b];
     const uint32_t r0 = a.r0[b];
-    const int64_t c = g / a.K;
     const int len = (int)min((int64_t)a.T, a.N_proc - g * a.T);
-    const int32_t p = a.off[b][g];
-    int32_t k = p / a.U, o = p - k * a.U;  // super-tile and row of the next active frame
-    const int64_t base = c * a.SPC;
+    const uint32_t p = (uint32_t)a.off[b][g];
+    uint32_t k = p / U, o = p - k * U;  // super-tile and row of the next active frame
+    const uint32_t base = (uint32_t)(g / a.K) * (uint32_t)a.SPC;
+    uint32_t idx = o * GS + base + k;  // its element
+    const uint32_t dummy = U * GS + g32 % GS;
     double *Mc = a.Mc[b];
-    // inactive frames store into this lane's own padding slot (row U of the
-    // array), so every store is unconditional and the pipeline stays counted
-    double *dummy = Mc + (int64_t)a.U * a.GS + g % a.GS;
     stream2<8, 2, uint16_t, double>(
-        len, [&](int i) { return R[(int64_t)min(i, len - 1) * a.G + g]; },
+        len, [&](int i) { return R[(uint32_t)min(i, len - 1) * G32]; },
         [&](uint16_t r) { return lut[r]; },
         [&](uint16_t r, double m) {
             const bool act = r >= r0;
-            double *dst = act ? Mc + (int64_t)o * a.GS + base + k : dummy;
-            *dst = m;
-            if (act && ++o == a.U) {
-                o = 0;
-                ++k;
-            }
+            Mc[act ? idx : dummy] = m;
+            const uint32_t o1 = o + (act ? 1u : 0u);
+            const bool wrap = o1 == U;
+            idx = act ? (wrap ? base + k + 1u : idx + GS) : idx;
+            k += wrap ? 1u : 0u;
+            o = wrap ? 0u : o1;
         });
 }
 

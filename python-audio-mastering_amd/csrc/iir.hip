@@ -284,7 +284,7 @@ __global__ void __launch_bounds__(LB_THREADS, 4) xover_kernel(XoArgs a, LbArgs l
         z[2 * k + 1] = zs[k][1];
         rst[2 * k] = rst[2 * k + 1] = 0.0;
     }
-    lb_carry<8, CH>(lb, blk, t, c, valid, valid && (g % line_tiles) == 0, rst, z, s, smem);
+    lb_carry<8, CH, 2>(lb, blk, t, c, valid, valid && (g % line_tiles) == 0, rst, z, s, smem);  // LP | HP branches
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         zs[k][0] = s[2 * k];

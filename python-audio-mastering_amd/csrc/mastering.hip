@@ -205,7 +205,7 @@ static int lb_prepare(mm_ctx *c, int64_t nblk, int ch, LbArgs &lb) {
 static int validate(mm_ctx *c, const mm_job *j) {
     if (!j) return set_err(c, MM_ERR_ARG, "null job");
     if (j->channels != 1 && j->channels != 2) return set_err(c, MM_ERR_ARG, "channels must be 1 or 2");
-    if (j->tile < 16 || j->tile > 4096) return set_err(c, MM_ERR_ARG, "tile %d out of range", j->tile);
+    if (j->tile < 16 || j->tile > 512) return set_err(c, MM_ERR_ARG, "tile %d out of range [16, 512]", j->tile);
     if (j->tiles_per_chunk < 1) return set_err(c, MM_ERR_ARG, "tiles_per_chunk < 1");
     if (j->frames_proc < 0 || j->frames_in < 0) return set_err(c, MM_ERR_ARG, "negative frame count");
     if (j->frames_proc >= (int64_t)1 << 31 || j->frames_in >= (int64_t)1 << 31)
