@@ -43,6 +43,12 @@ P_FULL = {"bass_boost": 4.0, "mid_cut": 3.0, "presence_boost": 1.0, "treble_boos
           "saturation": 30, "width": 1.3, "multiband": True, "lufs": -14.0}
 
 
+ENVELOPE_NOTE = ("the compressor envelope is a sequential non-linear recurrence solved exactly by speculative "
+                 "super-tile walks (one lane each, ~0.4 waves per SIMD): VALU-issue and dependent-latency bound, "
+                 "not HBM bound; the warm-up re-reads each M from the memory fabric ~7x (PMC traffic) "
+                 "(DESIGN.md §4)")
+
+
 def algorithmic_bytes(kernel, n, g, active, walked_per_launch):
     """Minimum HBM bytes one launch must move for its own inputs/outputs (stereo,
     n frames, g tiles, `active` compressor frames over the 3 bands)."""
@@ -186,8 +192,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS if achieved is not None else None,
                          "traffic": traffic, "algorithmic_bytes_per_launch": bpl,
                          "avg_launch_ms": avg_s * 1e3, "launches_per_step": launches,
-                         "note": "dominant kernel by device time; comp_fix is a latency-bound sequential "
-                                 "envelope walk (DESIGN.md §4)" if dom == "comp_fix" else None},
+                         "note": ENVELOPE_NOTE if dom in ("comp_pass0", "comp_fix", "comp_record") else None},
             "chain": {"algorithmic_bytes_per_frame": 16, "device_ms_per_step": dev_ms,
                       "achieved_GBps": 16 * job.frames_proc / (dt / args.steps) / 1e9,
                       "frac_of_peak": 16 * job.frames_proc / (dt / args.steps) / 1e9 / HBM_PEAK_GBS,

@@ -266,7 +266,7 @@ static int launch_eq(mm_ctx *c, int nsec, int ch, unsigned nblk, const EqArgs &e
 // at once if sweep k-1 changed nothing (so after the first quiet sweep both end
 // buffers hold the converged ends).  Convergence is checked at the chain's
 // single sync (comp_check); a rare unconverged batch is extended there.
-constexpr int COMP_SWEEPS = 4;
+constexpr int COMP_SWEEPS = 6;  // queued per chain; more resume from the host (re-compact + sweeps)
 
 static int comp_sweeps(mm_ctx *c, int n, bool resume = false) {
     CompArgs &ca = c->ca;
