@@ -263,17 +263,24 @@ __device__ __forceinline__ double lean_step(double att, double m, double inc, do
 // uses them, so they issue while the att chain of earlier frames is in flight
 // (in-order issue: tools/micro/walk2_bench.hip, 136 -> 98 cycles per step).
 // With STORE, overwrite each compacted M with the att after that frame.
+constexpr int WALK_WB = 32;  // M values in flight per walker
+constexpr int WALK_PAD = WALK_WB;  // padding rows after the compacted array (prefetch past a super-tile's end)
+
 template <bool STORE>
 __device__ __forceinline__ double comp_walk(double att, const CompArgs &a, int b, int64_t s, int len,
                                             const BandStep &bs) {
-    constexpr int WB = 32, WP = 4;
+    constexpr int WB = WALK_WB, WP = 4;
     if (len <= 0) return att;
-    double *col = a.Mc[b] + s;  // column s, rows GS apart (compacted frames < 2^31 / GS rows)
-    const uint32_t GS = (uint32_t)a.GS;
-    const int last = len - 1;
+    // column s, rows GS apart; loads run up to WB rows past the end (padding rows)
+    const size_t GS = (size_t)a.GS;
+    const double *pl = a.Mc[b] + s;
+    double *ps = a.Mc[b] + s;
     double buf[WB], inc[WP], dec[WP];
 #pragma unroll
-    for (int k = 0; k < WB; ++k) buf[k] = col[(uint32_t)min(k, last) * GS];
+    for (int k = 0; k < WB; ++k) {
+        buf[k] = *pl;
+        pl += GS;
+    }
 #pragma unroll
     for (int k = 0; k < WP; ++k) {
         inc[k] = div_cr(buf[k], bs.A, bs.rA);
@@ -288,8 +295,12 @@ __device__ __forceinline__ double comp_walk(double att, const CompArgs &a, int b
             inc[k % WP] = div_cr(mn, bs.A, bs.rA);
             dec[k % WP] = div_cr(mn, bs.R, bs.rR);
             att = lean_step(att, m, ik, dk);
-            if (STORE) col[(uint32_t)(i + k) * GS] = att;
-            buf[k] = col[(uint32_t)min(i + WB + k, last) * GS];
+            if (STORE) {
+                *ps = att;
+                ps += GS;
+            }
+            buf[k] = *pl;
+            pl += GS;
         }
     }
     const int rem = len - i;
@@ -301,7 +312,10 @@ __device__ __forceinline__ double comp_walk(double att, const CompArgs &a, int b
             inc[k % WP] = div_cr(mn, bs.A, bs.rA);
             dec[k % WP] = div_cr(mn, bs.R, bs.rR);
             att = lean_step(att, m, ik, dk);
-            if (STORE) col[(uint32_t)(i + k) * GS] = att;
+            if (STORE) {
+                *ps = att;
+                ps += GS;
+            }
         }
     }
     return att;

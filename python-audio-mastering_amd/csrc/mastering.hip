@@ -428,7 +428,7 @@ static int stage_front(mm_ctx *c, const mm_job *j, const float *d_in) {
             snprintf(nm, sizeof nm, "comp_r%d", b);
             RET(get_buf(c, nm, TG, &rb));
             snprintf(nm, sizeof nm, "comp_mc%d", b);
-            RET(get_buf(c, nm, (size_t)NS * (ca.U + 1), &mcb));  // + one padding row
+            RET(get_buf(c, nm, (size_t)NS * (ca.U + 1 + WALK_PAD), &mcb));  // + compaction dummy row + walk prefetch rows
             ca.r16[b] = rb;
             ca.Mc[b] = mcb;
             ca.band[b] = bands[b];
