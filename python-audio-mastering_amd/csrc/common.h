@@ -9,6 +9,11 @@
 
 namespace mm {
 
+// Workgroup barrier that orders LDS only.  __syncthreads()' fence also waits for
+// every outstanding global access (vmcnt(0)), i.e. it stalls on the block's own
+// in-flight stores and drains register prefetch pipelines at every barrier.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // Software-pipelined sequential stream over elements 0..len-1: ld(i) returns
 // element i and MUST be safe (clamped) for any i < len + NB*B; proc(v) consumes
 // elements in order.  NB*B elements stay in flight in registers, hiding

@@ -175,13 +175,14 @@ __global__ void __launch_bounds__(256) comp_compact_kernel(CompArgs a) {
         len, [&](int i) { return R[(uint32_t)min(i, len - 1) * G32]; },
         [&](uint16_t r) { return lut[r]; },
         [&](uint16_t r, double m) {
-            const bool act = r >= r0;
-            Mc[act ? idx : dummy] = m;
-            const uint32_t o1 = o + (act ? 1u : 0u);
-            const bool wrap = o1 == U;
-            idx = act ? (wrap ? base + k + 1u : idx + GS) : idx;
-            k += wrap ? 1u : 0u;
-            o = wrap ? 0u : o1;
+            // mask arithmetic: the compiler would turn selects into exec-mask branches
+            const uint32_t act = (uint32_t)r >= r0 ? 1u : 0u, amask = 0u - act;
+            Mc[(idx & amask) | (dummy & ~amask)] = m;
+            const uint32_t o1 = o + act;
+            const uint32_t wmask = 0u - (o1 == U ? 1u : 0u);  // the super-tile is full
+            idx = ((idx + (GS & amask)) & ~wmask) | ((base + k + 1u) & wmask);
+            k -= wmask;  // + 1 on a wrap
+            o = o1 & ~wmask;
         });
 }
 
@@ -536,7 +537,7 @@ __global__ void __launch_bounds__(192) comp_apply_kernel(CompArgs a) {
                 lds[b][j][lane] = s;
             }
         }
-        __syncthreads();
+        lds_barrier();
         for (int p = threadIdx.x; p < APPLY_STEP * APPLY_TILES; p += 3 * APPLY_TILES) {
             const int j = p / APPLY_TILES, tl = p % APPLY_TILES;
             const int64_t gt = g0 + tl;
@@ -548,7 +549,7 @@ __global__ void __launch_bounds__(192) comp_apply_kernel(CompArgs a) {
                 a.q_out[(int64_t)n * G + gt] = make_short2(l, a.ch == 2 ? rr : (int16_t)0);
             }
         }
-        __syncthreads();
+        lds_barrier();
     }
 }
 

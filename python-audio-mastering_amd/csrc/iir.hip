@@ -118,7 +118,7 @@ __device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, doub
     };
     load(0);
     store(0);
-    __syncthreads();
+    lds_barrier();
     const int64_t g = g0 + t;
     for (int step = 0; step < nsteps; ++step) {
         const int cur = step & 1;
@@ -147,7 +147,7 @@ __device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, doub
             }
         }
         if (step + 1 < nsteps) store(cur ^ 1);
-        __syncthreads();
+        lds_barrier();
     }
 }
 
