@@ -40,6 +40,9 @@ extern "C" {
 #define MM_OUT_I16 0 /* interleaved int16 PCM (what AME:89/98 writes)            */
 #define MM_OUT_F32 1 /* interleaved f32 = the same PCM / 32768 (decoded form)    */
 
+#define MM_IN_F32 0  /* input: interleaved f32 (decoded PCM16 / 32768)           */
+#define MM_IN_I16 1  /* input: interleaved int16 PCM, decoded (x / 32768) on the GPU */
+
 typedef struct mm_ctx mm_ctx;
 
 /* One IIR stage = 1..2 branches of cascaded DF2T biquads fed by the same input.
@@ -101,7 +104,7 @@ typedef struct mm_job {
     int32_t comp_warmup;     /* super-tiles of speculative warm-up walk before each one */
     int32_t comp_max_iters;  /* cap on fix-up sweeps (exactness check)          */
     int32_t comp_super;      /* frames per super-tile of the envelope solve (rounded to whole tiles) */
-    int32_t _pad2;
+    int32_t in_kind;         /* MM_IN_F32 (0) or MM_IN_I16                      */
     /* loudness geometry (pyloudnorm integrated_loudness, block 0.4 s, step 0.1 s) */
     int64_t n_blocks;
     const int64_t *block_lo; /* host [n_blocks] first frame of each block        */
@@ -129,16 +132,36 @@ int mm_sync(mm_ctx *ctx);
 int mm_version(void);
 
 /* ---- whole chain -------------------------------------------------------- */
-/* Host buffers: in = interleaved f32 [frames_in*channels] (PCM16/32768),
- * out = [frames_proc*channels] of out_kind.  Replaces AME:43-98 minus file/GCS IO. */
-int mm_master(mm_ctx *ctx, const mm_job *job, const float *in, void *out, mm_result *res);
+/* Host buffers: in = interleaved [frames_in*channels] of job->in_kind (f32 =
+ * PCM16/32768, or int16 PCM), out = [frames_proc*channels] of out_kind.
+ * Replaces AME:43-98 minus file/GCS IO. */
+int mm_master(mm_ctx *ctx, const mm_job *job, const void *in, void *out, mm_result *res);
 /* Same, with device-resident input/output (zero-copy; e.g. torch tensors). */
-int mm_master_device(mm_ctx *ctx, const mm_job *job, const float *d_in, void *d_out, mm_result *res);
+int mm_master_device(mm_ctx *ctx, const mm_job *job, const void *d_in, void *d_out, mm_result *res);
+
+/* ---- WAV files (AME:43 decode, AME:98 export) ------------------------------ */
+typedef struct mm_wav_info {
+    int64_t frames;          /* whole frames in the data chunk                   */
+    int64_t data_offset;     /* byte offset of the samples in the file           */
+    int32_t rate;
+    int32_t channels;
+    int32_t format;          /* 1 = PCM16, 3 = IEEE float32 (EXTENSIBLE resolved) */
+    int32_t bits;
+} mm_wav_info;
+/* Parse a RIFF/WAVE header (PCM16 or float32).  ctx may be NULL (no message). */
+int mm_wav_probe(mm_ctx *ctx, const char *path, mm_wav_info *info);
+/* Master a WAV file into out_path (PCM16 WAV for MM_OUT_I16, float32 WAV for
+ * MM_OUT_F32).  The samples stream from the file through pinned, double-buffered
+ * staging into HBM as they are read (PCM16 stays int16 across PCIe and is
+ * decoded on the GPU) and the output streams back the same way.  job must be
+ * built for the probed frames/rate/channels; its in_kind is ignored (taken from
+ * the file). */
+int mm_master_wav(mm_ctx *ctx, const mm_job *job, const char *in_path, const char *out_path, mm_result *res);
 
 /* ---- staged entry points (time-sharded multi-GPU, parity probes) -------- */
 /* Run AME:48-80 for this job's chunks into the context's int16 mix buffer and
  * the K-weighting per-tile aggregates (state carry-in assumed 0). */
-int mm_stage_chunks(mm_ctx *ctx, const mm_job *job, const float *d_in);
+int mm_stage_chunks(mm_ctx *ctx, const mm_job *job, const void *d_in);
 /* K-weighting end state of this job's range from a zero start: dim doubles. */
 int mm_kweight_range_end(mm_ctx *ctx, double *end_state_host);
 /* Per-segment K-weighted energies given a carry-in state (host [dim] or NULL);

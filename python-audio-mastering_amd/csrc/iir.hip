@@ -52,7 +52,8 @@ __device__ __forceinline__ double df2t(double x, double &z0, double &z1, const d
 constexpr int EQ_STAGE = 16;  // frames per tile staged through LDS per step
 
 struct EqArgs {
-    const float *in;   // natural interleaved f32 input
+    const float *in;   // natural interleaved f32 input (or null when in16 is set)
+    const int16_t *in16;  // natural interleaved int16 PCM input, decoded as x / 32768
     int64_t N_in;      // valid input frames (later frames read as 0: pydub pads)
     int64_t N_proc;    // processed frames
     int64_t G;         // tiles
@@ -96,7 +97,15 @@ __device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, doub
             const int64_t f = (g0 + tt) * T + n;
             const bool ok = n < T && f < a.N_in;  // also excludes tiles past the track end
             const int64_t fc = ok ? f : 0;
-            if constexpr (CH == 2) {
+            if (a.in16) {  // int16 -> f32 / 32768 is exact (AME:117-121)
+                if constexpr (CH == 2) {
+                    const short2 v = *reinterpret_cast<const short2 *>(a.in16 + 2 * fc);
+                    regs[r][0] = ok ? (float)v.x * (1.0f / 32768.0f) : 0.f;
+                    regs[r][1] = ok ? (float)v.y * (1.0f / 32768.0f) : 0.f;
+                } else {
+                    regs[r][0] = ok ? (float)a.in16[fc] * (1.0f / 32768.0f) : 0.f;
+                }
+            } else if constexpr (CH == 2) {
                 const float2 v = *reinterpret_cast<const float2 *>(a.in + 2 * fc);
                 regs[r][0] = ok ? v.x : 0.f;
                 regs[r][1] = ok ? v.y : 0.f;
@@ -198,7 +207,10 @@ __global__ void __launch_bounds__(256) pre_pointwise_kernel(EqArgs a) {
     const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= a.N_proc) return;
     float v[2] = {0.f, 0.f};
-    if (f < a.N_in) {
+    if (f < a.N_in && a.in16) {
+        v[0] = (float)a.in16[CH * f] * (1.0f / 32768.0f);
+        if constexpr (CH == 2) v[1] = (float)a.in16[2 * f + 1] * (1.0f / 32768.0f);
+    } else if (f < a.N_in) {
         if constexpr (CH == 2) {
             const float2 x = *reinterpret_cast<const float2 *>(a.in + 2 * f);
             v[0] = x.x;

@@ -65,6 +65,9 @@ struct mm_ctx {
     bool timing = false;
     std::vector<PendingEvent> pending;
     std::vector<hipEvent_t> free_events;
+    // pinned double-buffered staging for the WAV file path (mm_master_wav)
+    char *pin[2] = {nullptr, nullptr};
+    hipEvent_t pin_ev[2] = {nullptr, nullptr};
     std::map<std::string, KStat> stats;
     std::vector<std::string> stat_order;
     // host tables already resident on the device
@@ -205,6 +208,7 @@ static int lb_prepare(mm_ctx *c, int64_t nblk, int ch, LbArgs &lb) {
 static int validate(mm_ctx *c, const mm_job *j) {
     if (!j) return set_err(c, MM_ERR_ARG, "null job");
     if (j->channels != 1 && j->channels != 2) return set_err(c, MM_ERR_ARG, "channels must be 1 or 2");
+    if (j->in_kind != MM_IN_F32 && j->in_kind != MM_IN_I16) return set_err(c, MM_ERR_ARG, "in_kind %d", j->in_kind);
     if (j->tile < 16 || j->tile > 512) return set_err(c, MM_ERR_ARG, "tile %d out of range [16, 512]", j->tile);
     if (j->tiles_per_chunk < 1) return set_err(c, MM_ERR_ARG, "tiles_per_chunk < 1");
     if (j->frames_proc < 0 || j->frames_in < 0) return set_err(c, MM_ERR_ARG, "negative frame count");
@@ -323,7 +327,7 @@ static int chain_check(mm_ctx *c, bool *converged) {
 }
 
 // ------------------------------------------------------------ chain A..C
-static int stage_front(mm_ctx *c, const mm_job *j, const float *d_in) {
+static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
     RET(validate(c, j));
     const int T = j->tile, ch = j->channels, K = j->tiles_per_chunk;
     const int64_t N = j->frames_proc;
@@ -340,7 +344,8 @@ static int stage_front(mm_ctx *c, const mm_job *j, const float *d_in) {
     const unsigned nblk = blocks_for(std::max<int64_t>(G, 1), tpb);
 
     EqArgs ea{};
-    ea.in = d_in;
+    ea.in = j->in_kind == MM_IN_I16 ? nullptr : static_cast<const float *>(d_in);
+    ea.in16 = j->in_kind == MM_IN_I16 ? static_cast<const int16_t *>(d_in) : nullptr;
     ea.N_in = j->frames_in;
     ea.N_proc = N;
     ea.G = G;
@@ -641,7 +646,7 @@ static int finalize(mm_ctx *c, double gain, const double *gain_dev, int use_gain
 // The chain is queued without host round trips; one sync at the end checks
 // the compressor's convergence (a rare unconverged batch is extended and the
 // dependent stages re-run) and fetches the loudness.
-static int master_device(mm_ctx *c, const mm_job *j, const float *d_in, void *d_out, mm_result *res) {
+static int master_device(mm_ctx *c, const mm_job *j, const void *d_in, void *d_out, mm_result *res) {
     RET(stage_front(c, j, d_in));
     const bool lufs = j->lufs_on && c->G > 0;
     for (;;) {
@@ -682,7 +687,7 @@ static int master_device(mm_ctx *c, const mm_job *j, const float *d_in, void *d_
 }
 
 // Stage the chunk chain of a range (time-sharded ranks) to convergence.
-static int stage_chunks(mm_ctx *c, const mm_job *j, const float *d_in) {
+static int stage_chunks(mm_ctx *c, const mm_job *j, const void *d_in) {
     RET(stage_front(c, j, d_in));
     for (;;) {
         bool converged;
@@ -724,6 +729,10 @@ int mm_destroy(mm_ctx *c) {
     for (auto e : c->free_events) hipEventDestroy(e);
     for (auto &kv : c->bufs)
         if (kv.second.p) hipFree(kv.second.p);
+    for (int b = 0; b < 2; ++b) {
+        if (c->pin[b]) hipHostFree(c->pin[b]);
+        if (c->pin_ev[b]) hipEventDestroy(c->pin_ev[b]);
+    }
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
     return MM_OK;
@@ -738,25 +747,25 @@ int mm_sync(mm_ctx *c) {
     return MM_OK;
 }
 
-int mm_master_device(mm_ctx *c, const mm_job *j, const float *d_in, void *d_out, mm_result *res) {
+int mm_master_device(mm_ctx *c, const mm_job *j, const void *d_in, void *d_out, mm_result *res) {
     if (!c) return MM_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
     return master_device(c, j, d_in, d_out, res);
 }
 
-int mm_master(mm_ctx *c, const mm_job *j, const float *in, void *out, mm_result *res) {
+int mm_master(mm_ctx *c, const mm_job *j, const void *in, void *out, mm_result *res) {
     if (!c) return MM_ERR_ARG;
     RET(validate(c, j));
     HIPCHK(c, hipSetDevice(c->device));
-    float *d_in;
+    char *d_in;
     void *d_out;
-    const size_t in_n = (size_t)j->frames_in * j->channels;
+    const size_t in_bytes = (size_t)j->frames_in * j->channels * (j->in_kind == MM_IN_I16 ? 2 : 4);
     const size_t out_bytes = (size_t)j->frames_proc * j->channels * (j->out_kind == MM_OUT_I16 ? 2 : 4);
-    RET(get_buf(c, "host_in", std::max<size_t>(in_n, 1), &d_in));
+    RET(get_buf(c, "host_in", std::max<size_t>(in_bytes, 1), &d_in));
     char *ob;
     RET(get_buf(c, "host_out", std::max<size_t>(out_bytes, 1), &ob));
     d_out = ob;
-    if (in_n) HIPCHK(c, hipMemcpyAsync(d_in, in, in_n * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    if (in_bytes) HIPCHK(c, hipMemcpyAsync(d_in, in, in_bytes, hipMemcpyHostToDevice, c->stream));
     RET(master_device(c, j, d_in, d_out, res));
     if (out_bytes) HIPCHK(c, hipMemcpyAsync(out, d_out, out_bytes, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -764,7 +773,167 @@ int mm_master(mm_ctx *c, const mm_job *j, const float *in, void *out, mm_result 
     return MM_OK;
 }
 
-int mm_stage_chunks(mm_ctx *c, const mm_job *j, const float *d_in) {
+// ------------------------------------------------------------ WAV files
+// RIFF/WAVE codec of the file path (replaces pydub/ffmpeg decode, AME:43, and the
+// stdlib `wave` export, AME:98), mirroring mastering_amd/wavio.py: PCM16 or
+// IEEE float32 (WAVE_FORMAT_EXTENSIBLE resolved through its subformat), the
+// last fmt/data chunk wins, a data chunk running past the end of the file is
+// truncated to whole frames.
+static uint32_t le32(const unsigned char *p) { return p[0] | p[1] << 8 | p[2] << 16 | (uint32_t)p[3] << 24; }
+static uint16_t le16(const unsigned char *p) { return (uint16_t)(p[0] | p[1] << 8); }
+
+static int wav_parse(mm_ctx *c, FILE *f, const char *path, mm_wav_info *info) {
+    unsigned char h[40];
+    if (fseeko(f, 0, SEEK_END) != 0) return set_err(c, MM_ERR_ARG, "%s: cannot seek", path);
+    const int64_t fsize = (int64_t)ftello(f);
+    if (fseeko(f, 0, SEEK_SET) != 0 || fread(h, 1, 12, f) != 12 || memcmp(h, "RIFF", 4) || memcmp(h + 8, "WAVE", 4))
+        return set_err(c, MM_ERR_ARG, "%s: not a RIFF/WAVE file", path);
+    int64_t pos = 12, data_off = -1, data_size = 0;
+    int tag = -1, ch = 0, rate = 0, bits = 0;
+    while (pos + 8 <= fsize) {
+        if (fseeko(f, pos, SEEK_SET) != 0 || fread(h, 1, 8, f) != 8) break;
+        const int64_t size = le32(h + 4);
+        if (!memcmp(h, "fmt ", 4)) {
+            const size_t nb = (size_t)std::min<int64_t>(std::min<int64_t>(size, 40), fsize - pos - 8);
+            unsigned char b[40] = {0};
+            if (nb < 16 || fread(b, 1, nb, f) != nb) return set_err(c, MM_ERR_ARG, "%s: short fmt chunk", path);
+            tag = le16(b);
+            ch = le16(b + 2);
+            rate = (int)le32(b + 4);
+            bits = le16(b + 14);
+            if (tag == 0xFFFE && nb >= 26) tag = le16(b + 24);
+        } else if (!memcmp(h, "data", 4)) {
+            data_off = pos + 8;
+            data_size = std::min<int64_t>(size, fsize - data_off);
+        }
+        pos += 8 + size + (size & 1);
+    }
+    if (tag < 0 || data_off < 0) return set_err(c, MM_ERR_ARG, "%s: missing fmt or data chunk", path);
+    if (!((tag == 1 && bits == 16) || (tag == 3 && bits == 32)))
+        return set_err(c, MM_ERR_ARG, "%s: unsupported WAV format tag=%d bits=%d", path, tag, bits);
+    if (ch < 1 || rate < 1) return set_err(c, MM_ERR_ARG, "%s: bad fmt chunk (channels %d, rate %d)", path, ch, rate);
+    info->frames = data_size / (ch * bits / 8);
+    info->data_offset = data_off;
+    info->rate = rate;
+    info->channels = ch;
+    info->format = tag;
+    info->bits = bits;
+    return MM_OK;
+}
+
+int mm_wav_probe(mm_ctx *c, const char *path, mm_wav_info *info) {
+    if (!path || !info) return set_err(c, MM_ERR_ARG, "null argument");
+    FILE *f = fopen(path, "rb");
+    if (!f) return set_err(c, MM_ERR_ARG, "%s: cannot open", path);
+    const int rc = wav_parse(c, f, path, info);
+    fclose(f);
+    return rc;
+}
+
+constexpr size_t PIN_CHUNK = (size_t)8 << 20;  // bytes per staging buffer
+
+static int ensure_pinned(mm_ctx *c) {
+    for (int b = 0; b < 2; ++b) {
+        if (!c->pin[b]) HIPCHK(c, hipHostMalloc((void **)&c->pin[b], PIN_CHUNK, hipHostMallocDefault));
+        if (!c->pin_ev[b]) HIPCHK(c, hipEventCreateWithFlags(&c->pin_ev[b], hipEventDisableTiming));
+    }
+    return MM_OK;
+}
+
+namespace {
+struct FileCloser {
+    FILE *f;
+    ~FileCloser() {
+        if (f) fclose(f);
+    }
+};
+}  // namespace
+
+int mm_master_wav(mm_ctx *c, const mm_job *jin, const char *in_path, const char *out_path, mm_result *res) {
+    if (!c) return MM_ERR_ARG;
+    if (!jin || !in_path || !out_path) return set_err(c, MM_ERR_ARG, "null argument");
+    HIPCHK(c, hipSetDevice(c->device));
+    FileCloser in{fopen(in_path, "rb")};
+    if (!in.f) return set_err(c, MM_ERR_ARG, "%s: cannot open", in_path);
+    mm_wav_info wi;
+    RET(wav_parse(c, in.f, in_path, &wi));
+    mm_job j = *jin;
+    j.in_kind = wi.format == 1 ? MM_IN_I16 : MM_IN_F32;
+    if (j.frames_in != wi.frames || j.channels != wi.channels || j.rate != wi.rate)
+        return set_err(c, MM_ERR_ARG, "%s: job built for %lld frames x %d ch @ %d Hz, file has %lld x %d @ %d", in_path,
+                       (long long)j.frames_in, j.channels, j.rate, (long long)wi.frames, wi.channels, wi.rate);
+    RET(validate(c, &j));
+    const size_t in_bytes = (size_t)wi.frames * wi.channels * (wi.bits / 8);
+    const size_t out_bytes = (size_t)j.frames_proc * j.channels * (j.out_kind == MM_OUT_I16 ? 2 : 4);
+    if (out_bytes > 0xFFFFFFFFull - 36) return set_err(c, MM_ERR_ARG, "output larger than a RIFF file can hold");
+    char *d_in, *d_out;
+    RET(get_buf(c, "host_in", std::max<size_t>(in_bytes, 1), &d_in));
+    RET(get_buf(c, "host_out", std::max<size_t>(out_bytes, 1), &d_out));
+    RET(ensure_pinned(c));
+    // file -> pinned -> HBM: chunk k is read while chunk k-1 is in flight
+    if (fseeko(in.f, wi.data_offset, SEEK_SET) != 0) return set_err(c, MM_ERR_ARG, "%s: cannot seek", in_path);
+    size_t k = 0;
+    for (size_t off = 0; off < in_bytes; ++k) {
+        const int b = (int)(k & 1);
+        const size_t n = std::min(PIN_CHUNK, in_bytes - off);
+        if (k >= 2) HIPCHK(c, hipEventSynchronize(c->pin_ev[b]));
+        if (fread(c->pin[b], 1, n, in.f) != n) return set_err(c, MM_ERR_ARG, "%s: short read", in_path);
+        HIPCHK(c, hipMemcpyAsync(d_in + off, c->pin[b], n, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipEventRecord(c->pin_ev[b], c->stream));
+        off += n;
+    }
+    RET(master_device(c, &j, d_in, d_out, res));
+    // HBM -> pinned -> file: chunk k is written while chunk k+1 is copied back
+    FileCloser out{fopen(out_path, "wb")};
+    if (!out.f) return set_err(c, MM_ERR_ARG, "%s: cannot create", out_path);
+    const int tag = j.out_kind == MM_OUT_I16 ? 1 : 3, bits = j.out_kind == MM_OUT_I16 ? 16 : 32;
+    const int ba = j.channels * bits / 8;
+    unsigned char hdr[44];
+    auto put32 = [&](int at, uint32_t v) {
+        for (int i = 0; i < 4; ++i) hdr[at + i] = (unsigned char)(v >> (8 * i));
+    };
+    auto put16 = [&](int at, uint32_t v) {
+        hdr[at] = (unsigned char)v;
+        hdr[at + 1] = (unsigned char)(v >> 8);
+    };
+    memcpy(hdr, "RIFF", 4);
+    put32(4, (uint32_t)(36 + out_bytes));
+    memcpy(hdr + 8, "WAVEfmt ", 8);
+    put32(16, 16);
+    put16(20, tag);
+    put16(22, j.channels);
+    put32(24, j.rate);
+    put32(28, (uint32_t)j.rate * ba);
+    put16(32, ba);
+    put16(34, bits);
+    memcpy(hdr + 36, "data", 4);
+    put32(40, (uint32_t)out_bytes);
+    if (fwrite(hdr, 1, 44, out.f) != 44) return set_err(c, MM_ERR_ARG, "%s: write failed", out_path);
+    size_t prev_n = 0;
+    k = 0;
+    for (size_t off = 0; off < out_bytes; ++k) {
+        const int b = (int)(k & 1);
+        const size_t n = std::min(PIN_CHUNK, out_bytes - off);
+        HIPCHK(c, hipMemcpyAsync(c->pin[b], d_out + off, n, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipEventRecord(c->pin_ev[b], c->stream));
+        if (k >= 1) {
+            HIPCHK(c, hipEventSynchronize(c->pin_ev[b ^ 1]));
+            if (fwrite(c->pin[b ^ 1], 1, prev_n, out.f) != prev_n) return set_err(c, MM_ERR_ARG, "%s: write failed", out_path);
+        }
+        prev_n = n;
+        off += n;
+    }
+    if (k >= 1) {
+        const int b = (int)((k - 1) & 1);
+        HIPCHK(c, hipEventSynchronize(c->pin_ev[b]));
+        if (fwrite(c->pin[b], 1, prev_n, out.f) != prev_n) return set_err(c, MM_ERR_ARG, "%s: write failed", out_path);
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    resolve_events(c);
+    return MM_OK;
+}
+
+int mm_stage_chunks(mm_ctx *c, const mm_job *j, const void *d_in) {
     if (!c) return MM_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
     return stage_chunks(c, j, d_in);

@@ -15,7 +15,7 @@ import os
 
 import numpy as np
 
-from . import design, native, wavio
+from . import design, native
 
 # AME:15-20, verbatim values and descriptions.
 EQ_PRESETS = {
@@ -150,13 +150,21 @@ class Job:
         ctypes.memmove(dst.phi_blk_pow, bp.ctypes.data, bp.nbytes)
 
 
-def _as_f32_interleaved(pcm: np.ndarray) -> np.ndarray:
-    """int16 PCM -> f32 /32768 (AME:117-121); f32 input is taken as decoded PCM."""
+def _device_input(pcm: np.ndarray):
+    """PCM as the library takes it: int16 stays int16 (decoded /32768 on the GPU,
+    AME:117-121; half the PCIe bytes), float32 is taken as decoded PCM."""
     if pcm.dtype == np.int16:
-        return np.ascontiguousarray(pcm.astype(np.float32) / 32768)
+        return np.ascontiguousarray(pcm), native.MM_IN_I16
     if pcm.dtype == np.float32:
-        return np.ascontiguousarray(pcm)
+        return np.ascontiguousarray(pcm), native.MM_IN_F32
     raise TypeError("PCM must be int16 or float32")
+
+
+def _info(job: "Job", res: native.MMResult) -> dict:
+    return {"loudness": res.loudness if job.job.lufs_on else None,
+            "gain_db": (float(job.job.lufs_target) - res.loudness) if job.job.lufs_on else None,
+            "gain_linear": res.gain_linear, "frames": job.frames_proc, "comp_iters": res.comp_iters,
+            "chunks": len(job.chunks), "tile": job.tile}
 
 
 def master_pcm(pcm: np.ndarray, rate: int, params: dict, out_kind: int = native.MM_OUT_I16, device: int = 0):
@@ -164,18 +172,22 @@ def master_pcm(pcm: np.ndarray, rate: int, params: dict, out_kind: int = native.
     Returns (out_pcm, info) with out_pcm int16 (or f32 = int16/32768)."""
     ch = 1 if pcm.ndim == 1 else pcm.shape[1]
     job = Job(pcm.shape[0], rate, ch, params, out_kind)
-    x = _as_f32_interleaved(pcm)
+    x, job.job.in_kind = _device_input(pcm)
     shape = (job.frames_proc,) if ch == 1 else (job.frames_proc, ch)
     out = np.empty(shape, np.int16 if out_kind == native.MM_OUT_I16 else np.float32)
     ctx = native.context(device)
     res = native.MMResult()
     ctx.check(ctx.lib.mm_master(ctx.ptr, ctypes.byref(job.job), x.ctypes.data_as(ctypes.c_void_p),
                                 out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(res)), "mm_master")
-    info = {"loudness": res.loudness if job.job.lufs_on else None,
-            "gain_db": (float(job.job.lufs_target) - res.loudness) if job.job.lufs_on else None,
-            "gain_linear": res.gain_linear, "frames": job.frames_proc, "comp_iters": res.comp_iters,
-            "chunks": len(job.chunks), "tile": job.tile}
-    return out, info
+    return out, _info(job, res)
+
+
+def wav_info(path: str, device: int = 0) -> native.MMWavInfo:
+    """RIFF/WAVE header of `path` (PCM16 or float32), parsed by the library."""
+    ctx = native.context(device)
+    info = native.MMWavInfo()
+    ctx.check(ctx.lib.mm_wav_probe(ctx.ptr, os.fsencode(path), ctypes.byref(info)), "mm_wav_probe")
+    return info
 
 
 def master_device(ctx: native.Context, job: Job, d_in: int, d_out: int, res: native.MMResult | None = None):
@@ -190,16 +202,22 @@ def master_device(ctx: native.Context, job: Job, d_in: int, d_out: int, res: nat
 def process(input_path: str, output_path: str, params: dict, device: int = 0, verbose: bool = False) -> dict:
     """Master `input_path` (16-bit PCM or 32-bit float WAV) into `output_path`
     (16-bit PCM WAV, as AME:98 exports; params['output_format']='f32' writes float).
-    Raises ValueError/RuntimeError like the reference (AME:110-113)."""
+    The file streams through pinned staging into HBM and back (mm_master_wav).
+    Raises ValueError for unreadable/unsupported input and RuntimeError for device
+    failures, like the reference (AME:110-113)."""
     params = dict(params or {})
-    pcm, rate = wavio.read_wav(input_path)
     fmt = params.pop("output_format", "pcm16")
     kind = native.MM_OUT_F32 if fmt == "f32" else native.MM_OUT_I16
+    wi = wav_info(input_path, device)
     if verbose:
-        print(f"Loaded {input_path}: {pcm.shape[0]} frames @ {rate} Hz")
-    out, info = master_pcm(pcm, rate, params, kind, device)
+        print(f"Loaded {input_path}: {wi.frames} frames @ {wi.rate} Hz")
+    job = Job(wi.frames, wi.rate, wi.channels, params, kind)
+    ctx = native.context(device)
+    res = native.MMResult()
+    ctx.check(ctx.lib.mm_master_wav(ctx.ptr, ctypes.byref(job.job), os.fsencode(input_path), os.fsencode(output_path),
+                                    ctypes.byref(res)), "mm_master_wav")
+    info = _info(job, res)
     if verbose and info["loudness"] is not None:
         print(f"Current loudness: {info['loudness']:.2f} LUFS. Applying {info['gain_db']:.2f} dB gain...")
-    wavio.write_wav(output_path, out, rate)
     info["output_path"] = os.path.abspath(output_path)
     return info

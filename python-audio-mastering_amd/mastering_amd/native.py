@@ -15,6 +15,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MM_LIB") or os.path.join(_HERE, "libmastering_amd.so")
 
 MM_OUT_I16, MM_OUT_F32 = 0, 1
+MM_IN_F32, MM_IN_I16 = 0, 1
+MM_ERR_ARG = -1
 MAX_DIM, TILE_POW, BLK_POW = 8, 8, 65
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
@@ -43,7 +45,7 @@ class MMJob(ctypes.Structure):
                 ("multiband_on", ctypes.c_int32), ("lufs_on", ctypes.c_int32), ("out_kind", ctypes.c_int32),
                 ("lufs_target", ctypes.c_double), ("eq", MMIir), ("xover", MMIir), ("kweight", MMIir),
                 ("band", MMBand * 3), ("comp_warmup", ctypes.c_int32), ("comp_max_iters", ctypes.c_int32),
-                ("comp_super", ctypes.c_int32), ("_pad2", ctypes.c_int32),
+                ("comp_super", ctypes.c_int32), ("in_kind", ctypes.c_int32),
                 ("n_blocks", ctypes.c_int64), ("block_lo", c_int64_p), ("block_hi", c_int64_p),
                 ("n_segs", ctypes.c_int64), ("seg_bounds", c_int64_p), ("block_scale", ctypes.c_double)]
 
@@ -54,11 +56,16 @@ class MMResult(ctypes.Structure):
                 ("comp_active", ctypes.c_int64), ("comp_walked", ctypes.c_int64)]
 
 
+class MMWavInfo(ctypes.Structure):
+    _fields_ = [("frames", ctypes.c_int64), ("data_offset", ctypes.c_int64), ("rate", ctypes.c_int32),
+                ("channels", ctypes.c_int32), ("format", ctypes.c_int32), ("bits", ctypes.c_int32)]
+
+
 # every symbol include/mastering.h declares (checked by tests/test_abi.py)
 EXPORTS = ("mm_create", "mm_destroy", "mm_last_error", "mm_sync", "mm_version", "mm_master", "mm_master_device",
            "mm_stage_chunks", "mm_kweight_range_end", "mm_hop_energies", "mm_gate_loudness", "mm_finalize",
            "mm_read_mix", "mm_timing", "mm_kernel_stats", "mm_comm_unique_id", "mm_comm_init", "mm_comm_destroy",
-           "mm_allreduce_sum_f64", "mm_allgather_f64")
+           "mm_allreduce_sum_f64", "mm_allgather_f64", "mm_wav_probe", "mm_master_wav")
 
 _lib = None
 _lock = threading.Lock()
@@ -88,6 +95,8 @@ def load():
             "mm_master": ([vp, P(MMJob), vp, vp, P(MMResult)], ctypes.c_int),
             "mm_master_device": ([vp, P(MMJob), vp, vp, P(MMResult)], ctypes.c_int),
             "mm_stage_chunks": ([vp, P(MMJob), vp], ctypes.c_int),
+            "mm_wav_probe": ([vp, ctypes.c_char_p, P(MMWavInfo)], ctypes.c_int),
+            "mm_master_wav": ([vp, P(MMJob), ctypes.c_char_p, ctypes.c_char_p, P(MMResult)], ctypes.c_int),
             "mm_kweight_range_end": ([vp, c_double_p], ctypes.c_int),
             "mm_hop_energies": ([vp, c_double_p, c_double_p], ctypes.c_int),
             "mm_gate_loudness": ([P(MMJob), c_double_p, c_double_p], ctypes.c_int),
@@ -122,9 +131,12 @@ class Context:
         self.device = device
 
     def check(self, rc: int, what: str):
+        """Raise on a negative status: ValueError for bad arguments or input files
+        (MM_ERR_ARG, like the reference's decode errors), RuntimeError otherwise."""
         if rc < 0:
             msg = self.lib.mm_last_error(self.ptr)
-            raise RuntimeError(f"{what} failed ({rc}): {msg.decode(errors='replace') if msg else ''}")
+            text = f"{what} failed ({rc}): {msg.decode(errors='replace') if msg else ''}"
+            raise ValueError(text) if rc == MM_ERR_ARG else RuntimeError(text)
         return rc
 
     def close(self):

@@ -46,6 +46,7 @@ def test_struct_layouts_match_c(tmp_path):
         "mm_iir": [f[0] for f in native.MMIir._fields_],
         "mm_band": [f[0] for f in native.MMBand._fields_],
         "mm_result": [f[0] for f in native.MMResult._fields_],
+        "mm_wav_info": [f[0] for f in native.MMWavInfo._fields_],
     }
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "mastering.h"', "int main(void){"]
     for st, fl in fields.items():
@@ -58,7 +59,7 @@ def test_struct_layouts_match_c(tmp_path):
     subprocess.check_call(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)])
     got = dict(line.rsplit(" ", 1) for line in subprocess.check_output([str(exe)]).decode().splitlines())
     classes = {"mm_job": native.MMJob, "mm_iir": native.MMIir, "mm_band": native.MMBand,
-               "mm_result": native.MMResult}
+               "mm_result": native.MMResult, "mm_wav_info": native.MMWavInfo}
     for st, cls in classes.items():
         assert int(got[st]) == ctypes.sizeof(cls), st
         for f in fields[st]:
