@@ -478,7 +478,10 @@ __global__ void __launch_bounds__(256) comp_tstart_kernel(CompArgs a) {
 // trajectory from tstart for its 64 tiles (audioop.mul floor on both channels),
 // 8 frames at a time into LDS; then all 192 threads overlay
 // sat16(sat16(lo + mid) + hi) (AME:210) and store q2 coalesced.
-constexpr int APPLY_TILES = 64, APPLY_STEP = 8;
+#ifndef MM_APPLY_STEP
+#define MM_APPLY_STEP 8
+#endif
+constexpr int APPLY_TILES = 64, APPLY_STEP = MM_APPLY_STEP;
 
 // -att / 20, correctly rounded (Markstein with RN(1/20) = 0.05; checked
 // exhaustively on the attenuation range in tests/test_oracle.py)

@@ -49,7 +49,13 @@ __device__ __forceinline__ double df2t(double x, double &z0, double &z1, const d
 }
 
 // ------------------------------------------------------------------ EQ stage
-constexpr int EQ_STAGE = 16;  // frames per tile staged through LDS per step
+#ifndef MM_EQ_STAGE
+#define MM_EQ_STAGE 16
+#endif
+#ifndef MM_XO_NB
+#define MM_XO_NB 3
+#endif
+constexpr int EQ_STAGE = MM_EQ_STAGE;  // frames per tile staged through LDS per step
 
 struct EqArgs {
     const float *in;   // natural interleaved f32 input (or null when in16 is set)
@@ -78,7 +84,7 @@ constexpr int eq_lds_bytes() {
 // cooperatively loads EQ_STAGE frames of each of its tiles (16 consecutive
 // threads read one tile's 128 contiguous bytes), double-buffered so the next
 // stage's loads are in flight while lanes run the recurrence.
-template <int NS, int CH, bool P2>
+template <int NS, int CH, bool P2, bool I16>
 __device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, double (&z)[NS][2], float *stage) {
     constexpr int TPB = LB_THREADS / CH;
     constexpr int ROW = (EQ_STAGE + 1) * CH;       // floats per staged tile row (padded)
@@ -97,7 +103,7 @@ __device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, doub
             const int64_t f = (g0 + tt) * T + n;
             const bool ok = n < T && f < a.N_in;  // also excludes tiles past the track end
             const int64_t fc = ok ? f : 0;
-            if (a.in16) {  // int16 -> f32 / 32768 is exact (AME:117-121)
+            if constexpr (I16) {  // int16 -> f32 / 32768 is exact (AME:117-121)
                 if constexpr (CH == 2) {
                     const short2 v = *reinterpret_cast<const short2 *>(a.in16 + 2 * fc);
                     regs[r][0] = ok ? (float)v.x * (1.0f / 32768.0f) : 0.f;
@@ -160,7 +166,9 @@ __device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, doub
     }
 }
 
-template <int NS, int CH>
+// I16: the input is int16 PCM (a.in16), else f32 (a.in); a template parameter so
+// the staging loads carry no runtime branch (it costs registers and spills).
+template <int NS, int CH, bool I16>
 __global__ void __launch_bounds__(LB_THREADS, 4) eq_kernel(EqArgs a, LbArgs lb, int64_t line_tiles) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     constexpr int TPB = LB_THREADS / CH;
@@ -181,7 +189,7 @@ __global__ void __launch_bounds__(LB_THREADS, 4) eq_kernel(EqArgs a, LbArgs lb, 
     double zs[NS][2];
 #pragma unroll
     for (int s = 0; s < NS; ++s) zs[s][0] = zs[s][1] = 0.0;
-    eq_pass<NS, CH, false>(a, g0, t, c, len, zs, stage);
+    eq_pass<NS, CH, false, I16>(a, g0, t, c, len, zs, stage);
     double z[DIM], s[DIM], rst[DIM];
 #pragma unroll
     for (int s_ = 0; s_ < NS; ++s_) {
@@ -197,7 +205,7 @@ __global__ void __launch_bounds__(LB_THREADS, 4) eq_kernel(EqArgs a, LbArgs lb, 
         zs[s_][0] = s[2 * s_];
         zs[s_][1] = s[2 * s_ + 1];
     }
-    eq_pass<NS, CH, true>(a, g0, t, c, len, zs, stage);
+    eq_pass<NS, CH, true, I16>(a, g0, t, c, len, zs, stage);
 }
 
 // No active EQ stage: the chain stays f32 (AME:152-162 returns the f32 input;
@@ -250,7 +258,7 @@ __device__ __forceinline__ void xo_pass(const XoArgs &a, int64_t g, int c, int l
     const double(*sos)[5] = a.sos;
     const int64_t G = a.G;
     int pn = 0;
-    stream<8, 3, int16_t>(
+    stream<8, MM_XO_NB, int16_t>(
         len, [&](int i) { return a.q_in[((int64_t)min(i, len - 1) * G + g) * 2 + c]; },
         [&](int16_t q) {
             const double x = (double)((float)q / 32768.0f);  // AME:199 int16 -> f32

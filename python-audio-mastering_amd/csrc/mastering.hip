@@ -250,10 +250,12 @@ template <int NS>
 static int launch_eq_ns(mm_ctx *c, int ch, unsigned nblk, const EqArgs &ea, const LbArgs &lb, int64_t K) {
     if (ch == 2) {
         const size_t lds = eq_lds_bytes<NS, 2>();
-        return launch(c, "eq", eq_kernel<NS, 2>, dim3(nblk), dim3(LB_THREADS), lds, ea, lb, K);
+        if (ea.in16) return launch(c, "eq", eq_kernel<NS, 2, true>, dim3(nblk), dim3(LB_THREADS), lds, ea, lb, K);
+        return launch(c, "eq", eq_kernel<NS, 2, false>, dim3(nblk), dim3(LB_THREADS), lds, ea, lb, K);
     }
     const size_t lds = eq_lds_bytes<NS, 1>();
-    return launch(c, "eq", eq_kernel<NS, 1>, dim3(nblk), dim3(LB_THREADS), lds, ea, lb, K);
+    if (ea.in16) return launch(c, "eq", eq_kernel<NS, 1, true>, dim3(nblk), dim3(LB_THREADS), lds, ea, lb, K);
+    return launch(c, "eq", eq_kernel<NS, 1, false>, dim3(nblk), dim3(LB_THREADS), lds, ea, lb, K);
 }
 
 static int launch_eq(mm_ctx *c, int nsec, int ch, unsigned nblk, const EqArgs &ea, const LbArgs &lb, int64_t K) {
