@@ -167,3 +167,18 @@ def test_time_sharded_on_one_gpu(oracle):
     assert not errs, errs
     assert infos[0]["loudness"] == infos[1]["loudness"]
     _check(np.concatenate(outs), infos[0], ref, Lref)
+
+
+@pytest.mark.parametrize("warmup", [0, 1])
+def test_compressor_resume_path(oracle, monkeypatch, warmup):
+    """With little or no speculative warm-up the Jacobi sweeps need more than the
+    queued ones, so the host resumes (re-compact, more sweeps, back end again): the
+    result must still be exact against the oracle."""
+    from mastering_amd import engine, master_pcm
+    from mastering_amd.synth import pink_noise_pcm16
+    monkeypatch.setattr(engine, "COMP_WARMUP", warmup)
+    pcm = pink_noise_pcm16(40 * 44100, 44100, 2, 11)
+    out, info = master_pcm(pcm, 44100, P_HOT)
+    assert info["comp_iters"] > 6, info["comp_iters"]  # more than the 6 queued sweeps
+    ref, L = oracle.master(pcm, 44100, P_HOT, return_loudness=True)
+    _check(out, info, ref, L)
