@@ -49,6 +49,12 @@ struct mm_ctx {
     int64_t G = 0;
     short2 *mix = nullptr;
     unsigned *lb_error = nullptr;
+    // per-chain control words, zeroed by ONE memset at the chain start: the three
+    // IIR stages' ticket/status regions and the compressor's sweep flags; a
+    // region is "fresh" until its first use (repeats zero their own words)
+    unsigned *ctl_lb[3] = {nullptr, nullptr, nullptr};
+    bool ctl_fresh[3] = {false, false, false};
+    bool comp_flags_fresh = false;
     // compressor state kept across the queued launches (stage_front -> comp_sweeps/comp_back)
     bool comp_on = false;
     CompArgs ca{};
@@ -191,16 +197,26 @@ static int upload_tables(mm_ctx *c, const char *name, const mm_iir &f, LbArgs &l
 
 // Per-launch look-back state for nblk blocks of CH lines: the ticket and the
 // status words are zeroed by a memset on the stream right before the launch.
-static int lb_prepare(mm_ctx *c, int64_t nblk, int ch, LbArgs &lb) {
-    const size_t flag_bytes = ((16 + (size_t)nblk * 4) + 15) / 16 * 16;
+static size_t lb_flag_bytes(int64_t nblk) { return ((16 + (size_t)nblk * 4) + 15) / 16 * 16; }
+
+// region: the chain's pre-zeroed control region of this stage (0 eq, 1 crossover,
+// 2 K-weighting), used once; otherwise (or on a repeat) a private memset.
+static int lb_prepare(mm_ctx *c, int64_t nblk, int ch, LbArgs &lb, int region = -1) {
     char *flags;
-    RET(get_buf(c, "lb_flags", flag_bytes, &flags));
-    HIPCHK(c, hipMemsetAsync(flags, 0, flag_bytes, c->stream));
+    if (region >= 0 && c->ctl_fresh[region]) {
+        flags = reinterpret_cast<char *>(c->ctl_lb[region]);
+        c->ctl_fresh[region] = false;
+    } else {
+        const size_t flag_bytes = lb_flag_bytes(nblk);
+        RET(get_buf(c, "lb_flags", flag_bytes, &flags));
+        HIPCHK(c, hipMemsetAsync(flags, 0, flag_bytes, c->stream));
+    }
     lb.ticket = reinterpret_cast<unsigned *>(flags);
     lb.status = reinterpret_cast<unsigned *>(flags + 16);
     RET(get_buf(c, "lb_agg", (size_t)nblk * ch * 8, &lb.agg));
     RET(get_buf(c, "lb_incl", (size_t)nblk * ch * 8, &lb.incl));
-    RET(get_buf(c, "lb_error", 4, &lb.error));
+    if (c->lb_error) lb.error = c->lb_error;
+    else RET(get_buf(c, "lb_error", 4, &lb.error));
     lb.init = nullptr;
     return MM_OK;
 }
@@ -279,7 +295,9 @@ static int comp_sweeps(mm_ctx *c, int n, bool resume = false) {
     // comp_record overwrote Mc with attenuations: restore M before resuming
     if (resume) RET(launch(c, "comp_compact", comp_compact_kernel, dim3(c->comp_nb, 3), dim3(256), 0, ca));
     const int64_t NS = ca.GS;
-    HIPCHK(c, hipMemsetAsync(c->comp_changed, 0, 16 * sizeof(unsigned int), c->stream));  // flags only
+    if (!c->comp_flags_fresh)  // flags only (the walked count accumulates)
+        HIPCHK(c, hipMemsetAsync(c->comp_changed, 0, 16 * sizeof(unsigned int), c->stream));
+    c->comp_flags_fresh = false;
     for (int k = 0; k < n; ++k) {
         for (int b = 0; b < 3; ++b) {
             ca.end_in[b] = c->comp_cur + (size_t)b * NS;
@@ -340,10 +358,23 @@ static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
     c->staged = false;
     short2 *q1;
     RET(get_buf(c, "q1", TG, &q1));
-    RET(get_buf(c, "lb_error", 4, &c->lb_error));
-    HIPCHK(c, hipMemsetAsync(c->lb_error, 0, 4, c->stream));
     const int tpb = LB_THREADS / ch;
     const unsigned nblk = blocks_for(std::max<int64_t>(G, 1), tpb);
+    {  // control words of the whole chain: [0] look-back error, [64..128) sweep
+       // flags + walked count, then the eq / crossover / K-weighting regions
+        const size_t region = lb_flag_bytes(nblk);  // >= the K-weighting stage's (256 tiles per block)
+        const size_t bytes = 512 + 3 * region;
+        char *ctl;
+        RET(get_buf(c, "ctl", bytes, &ctl));
+        HIPCHK(c, hipMemsetAsync(ctl, 0, bytes, c->stream));
+        c->lb_error = reinterpret_cast<unsigned *>(ctl);
+        c->comp_changed = reinterpret_cast<unsigned *>(ctl + 256);
+        for (int r = 0; r < 3; ++r) {
+            c->ctl_lb[r] = reinterpret_cast<unsigned *>(ctl + 512 + r * region);
+            c->ctl_fresh[r] = true;
+        }
+        c->comp_flags_fresh = true;
+    }
 
     EqArgs ea{};
     ea.in = j->in_kind == MM_IN_I16 ? nullptr : static_cast<const float *>(d_in);
@@ -369,7 +400,7 @@ static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
             fill_sos(ea.sos, j->eq, j->eq.nsec);
             LbArgs lb{};
             RET(upload_tables(c, "eq", j->eq, lb));
-            RET(lb_prepare(c, nblk, ch, lb));
+            RET(lb_prepare(c, nblk, ch, lb, 0));
             RET(launch_eq(c, j->eq.nsec, ch, nblk, ea, lb, K));
         }
     }
@@ -390,7 +421,7 @@ static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
         for (int b = 0; b < 3; ++b) xa.band[b] = reinterpret_cast<int16_t *>(bands[b]);
         LbArgs lb{};
         RET(upload_tables(c, "xover", j->xover, lb));
-        RET(lb_prepare(c, nblk, ch, lb));
+        RET(lb_prepare(c, nblk, ch, lb, 1));
         if (ch == 2)
             RET(launch(c, "xover", xover_kernel<2>, dim3(nblk), dim3(LB_THREADS), lb_lds_bytes<8, 2>(), xa, lb,
                        (int64_t)K));
@@ -420,10 +451,8 @@ static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
         RET(get_buf(c, "comp_endB", (size_t)3 * NS, &eB));
         RET(get_buf(c, "comp_tstart", (size_t)3 * G, &tst));
         RET(get_buf(c, "comp_lut", (size_t)3 * 32769, &luts));
-        unsigned int *changed;
-        RET(get_buf(c, "comp_changed", 64, &changed));
+        unsigned int *changed = c->comp_changed;  // zeroed with the chain's control words
         ca.walked = reinterpret_cast<unsigned long long *>(changed + 32);
-        HIPCHK(c, hipMemsetAsync(ca.walked, 0, 8, c->stream));
         int32_t *cnt, *off, *tot;
         RET(get_buf(c, "comp_cnt", (size_t)3 * G, &cnt));
         RET(get_buf(c, "comp_off", (size_t)3 * G, &off));
@@ -532,7 +561,7 @@ static int kweight_launch(mm_ctx *c, const double *carry_in_host, double *line_e
     LbArgs lb{};
     RET(upload_tables(c, "kweight", j->kweight, lb));
     const unsigned nblk = blocks_for(G, LB_THREADS);
-    RET(lb_prepare(c, nblk, 1, lb));
+    RET(lb_prepare(c, nblk, 1, lb, 2));
     if (carry_in_host) {
         double *init;
         RET(get_buf(c, "kw_init", 8, &init));
