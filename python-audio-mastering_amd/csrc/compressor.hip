@@ -334,26 +334,50 @@ __device__ __forceinline__ double comp_walk_lean(double att, const CompArgs &a, 
     return att;
 }
 
-// 4. speculative pass.  grid: (ceil(GS/256), 3).  The start of super-tile s
-// is guessed by walking the `warmup` previous super-tiles of its chunk, from the
-// M of the first warm-up frame (the state tracks M closely: this coalesces with
-// the true trajectory far more often than a start at 0; tools/ studies).
-__global__ void __launch_bounds__(256) comp_pass0_kernel(CompArgs a) {
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// 4. speculative pass.  grid: (ceil(GS/(OWN*BLOCK)), 3).  Each lane walks OWN
+// consecutive super-tiles.  The start of the first is guessed by walking the
+// `warmup` previous super-tiles of its chunk, from the M of the first warm-up
+// frame (the state tracks M closely: this coalesces with the true trajectory far
+// more often than a start at 0; tools/ studies); the later ones start from the
+// end of the one before (a longer warm-up for free).  OWN > 1 divides the
+// warm-up walks (and their M re-reads) by OWN.
+#ifndef MM_PASS0_OWN
+#define MM_PASS0_OWN 2
+#endif
+#ifndef MM_PASS0_BLOCK
+#define MM_PASS0_BLOCK 64
+#endif
+constexpr int PASS0_OWN = MM_PASS0_OWN;
+constexpr int PASS0_BLOCK = MM_PASS0_BLOCK;
+
+__global__ void __launch_bounds__(PASS0_BLOCK) comp_pass0_kernel(CompArgs a) {
+    const int64_t s0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * PASS0_OWN;
     const int b = blockIdx.y;
-    if (s >= a.GS) return;
-    const Super st = super_of(a, b, s);
-    if (st.len == 0) return;
+    if (s0 >= a.GS) return;
     const BandStep bs = band_step(a, b);
     double att = 0.0;
-    if (a.warmup > 0 && st.p0 > 0) {
-        const int64_t k = st.p0 / a.U;  // index of s within its chunk
-        const int64_t w0 = s - min((int64_t)a.warmup, k);
-        att = a.Mc[b][w0];  // row 0 of super-tile w0
-        for (int64_t w = w0; w < s; ++w) att = comp_walk<false>(att, a, b, w, a.U, bs);
+    bool warm = false;
+    for (int64_t s = s0; s < min(s0 + PASS0_OWN, a.GS); ++s) {
+        const Super st = super_of(a, b, s);
+        if (st.len == 0) {
+            warm = false;
+            continue;
+        }
+        if (st.p0 == 0) {  // chunk start: exact
+            att = 0.0;
+        } else if (!warm && a.warmup > 0) {
+            const int64_t k = st.p0 / a.U;  // index of s within its chunk
+            const int64_t w0 = s - min((int64_t)a.warmup, k);
+            att = a.Mc[b][w0];  // row 0 of super-tile w0
+            for (int64_t w = w0; w < s; ++w) att = comp_walk<false>(att, a, b, w, a.U, bs);
+        } else if (!warm) {
+            att = 0.0;
+        }
+        a.start[b][s] = att;
+        att = comp_walk<false>(att, a, b, s, st.len, bs);
+        a.end_out[b][s] = att;
+        warm = true;
     }
-    a.start[b][s] = att;
-    a.end_out[b][s] = comp_walk<false>(att, a, b, s, st.len, bs);
 }
 
 // 5. one Jacobi sweep (exits at once if the previous sweep changed nothing).
@@ -449,7 +473,12 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
 }
 
 // 6. exact att after every active frame (Mc is overwritten in place).
-__global__ void __launch_bounds__(256) comp_record_kernel(CompArgs a) {
+#ifndef MM_RECORD_BLOCK
+#define MM_RECORD_BLOCK 256
+#endif
+constexpr int RECORD_BLOCK = MM_RECORD_BLOCK;  // lanes (super-tiles) per block: few blocks spread over more CUs
+
+__global__ void __launch_bounds__(RECORD_BLOCK) comp_record_kernel(CompArgs a) {
     const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int b = blockIdx.y;
     if (s >= a.GS) return;

@@ -61,7 +61,7 @@ struct mm_ctx {
     double *comp_cur = nullptr, *comp_nxt = nullptr;
     unsigned *comp_changed = nullptr;
     int comp_iters = 0, comp_pending = 0;
-    unsigned comp_nb = 0, comp_nbs = 0;
+    unsigned comp_nb = 0;
     // loudness on the device
     double *gate_out = nullptr;         // [2]: L, gain
     std::vector<int64_t> geom_cache;    // loudness geometry already on the device
@@ -316,7 +316,7 @@ static int comp_sweeps(mm_ctx *c, int n, bool resume = false) {
 // overlay into q2.
 static int comp_back(mm_ctx *c) {
     const CompArgs &ca = c->ca;
-    RET(launch(c, "comp_record", comp_record_kernel, dim3(c->comp_nbs, 3), dim3(256), 0, ca));
+    RET(launch(c, "comp_record", comp_record_kernel, dim3(blocks_for(ca.GS, RECORD_BLOCK), 3), dim3(RECORD_BLOCK), 0, ca));
     RET(launch(c, "comp_tstart", comp_tstart_kernel, dim3(c->comp_nb, 3), dim3(256), 0, ca));
     return launch(c, "comp_apply", comp_apply_kernel, dim3(blocks_for(ca.G, APPLY_TILES)), dim3(3 * APPLY_TILES), 0,
                   ca);
@@ -490,11 +490,11 @@ static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
             ca.tstart[b] = tst + (size_t)b * G;
             ca.end_out[b] = eA + (size_t)b * NS;
         }
-        const unsigned nbs = blocks_for(NS, 256);
         RET(launch(c, "comp_rms", comp_rms_kernel, dim3(nb, 3), dim3(256), 0, ca));
         RET(launch(c, "comp_offsets", comp_offsets_kernel, dim3((unsigned)nchunks, 3), dim3(1024), 0, ca));
         RET(launch(c, "comp_compact", comp_compact_kernel, dim3(nb, 3), dim3(256), 0, ca));
-        RET(launch(c, "comp_pass0", comp_pass0_kernel, dim3(nbs, 3), dim3(256), 0, ca));
+        RET(launch(c, "comp_pass0", comp_pass0_kernel,
+                   dim3(blocks_for((NS + PASS0_OWN - 1) / PASS0_OWN, PASS0_BLOCK), 3), dim3(PASS0_BLOCK), 0, ca));
         c->comp_on = true;
         c->ca = ca;
         c->comp_cur = eA;
@@ -503,7 +503,6 @@ static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
         c->comp_iters = 0;
         c->comp_pending = 0;
         c->comp_nb = nb;
-        c->comp_nbs = nbs;
         RET(comp_sweeps(c, COMP_SWEEPS));
         RET(comp_back(c));
         mix = q2;

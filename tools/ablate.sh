@@ -9,5 +9,5 @@ for lib in "" $(ls build/var/*.so 2>/dev/null); do
      > gpurun_out/abl.json 2> gpurun_out/abl.err || { echo "$name failed"; tail -5 gpurun_out/abl.err; exit 1; }
   python -c "
 import json,sys;d=json.load(open('gpurun_out/abl.json'));k=d['chain']['kernels_ms_per_step']
-print('$name'.ljust(28), round(d['ms_per_step'],3), ' '.join(f'{x}={k.get(x)}' for x in '$ks'.split()))"
+print('$name'.ljust(28), round(d['ms_per_step'],3), 'it', d['chain']['comp_iters'], 'rw', d['chain']['comp_rewalked_frames'], ' '.join(f'{x}={k.get(x)}' for x in '$ks'.split()))"
 done
