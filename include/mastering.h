@@ -181,6 +181,43 @@ int mm_timing(mm_ctx *ctx, int enable);
 /* names: '\n'-joined kernel names into buf; ms/launches arrays of cap entries. */
 int mm_kernel_stats(mm_ctx *ctx, char *names, int names_cap, double *total_ms, int64_t *launches, int cap);
 
+/* ---- per-stage operators (AME:117-227, one stage at a time) --------------
+ * The reference's public DSP helpers as standalone device operators, numpy in /
+ * numpy out through host buffers (mastering_amd/ops.py mirrors their Python
+ * signatures).  dtype is the sample type of a float input; an f32 input computes
+ * in f32 (numpy's dtype rules for the reference's expressions), an f64 one in f64.
+ * n counts samples, frames count [frames][channels] rows. */
+#define MM_F32 0
+#define MM_F64 1
+/* audio_segment_to_float_array (AME:117-121): int16 -> f32 / 32768 */
+int mm_op_pcm_to_float(mm_ctx *ctx, const int16_t *in, int64_t n, float *out);
+/* apply_saturation (AME:128-134); percent != 0 (0 is the identity, no call) */
+int mm_op_saturation(mm_ctx *ctx, int dtype, const void *in, int64_t n, double percent, void *out);
+/* apply_stereo_width (AME:136-144) on interleaved stereo [frames][2] */
+int mm_op_stereo_width(mm_ctx *ctx, int dtype, const void *in, int64_t frames, double width, void *out);
+/* float_array_to_audio_segment's samples (AME:123-126): clip, *32768, astype(int16) */
+int mm_op_quantize(mm_ctx *ctx, int dtype, const void *in, int64_t n, int16_t *out);
+/* soft_limiter (AME:224-227), in place like the reference */
+int mm_op_soft_limiter(mm_ctx *ctx, int dtype, void *inout, int64_t n, double threshold);
+/* samples * np.float64(gain) -> f64 (AME:222) */
+int mm_op_gain(mm_ctx *ctx, int dtype, const void *in, int64_t n, double gain, double *out);
+/* scipy.signal.sosfilt of ONE cascade (f->nsec 1..4 sections, all in branch 0,
+ * tables for LB tiles/block = 256/channels) over each channel column of
+ * [frames][channels], zero initial state; f64 out.  round_f32: every section's
+ * output is rounded to f32 (pyloudnorm's lfilter write-backs).  Replaces
+ * apply_eq_to_samples / apply_shelf_filter / apply_peak_filter (AME:146-194). */
+int mm_op_sosfilt(mm_ctx *ctx, int dtype, const void *in, int64_t frames, int channels, const mm_iir *f,
+                  int round_f32, double *out);
+/* pyloudnorm Meter(rate).integrated_loudness of samples.mean(axis=1) (AME:213-218).
+ * job: channels, frames_proc, kweight (tpb 256), loudness geometry, lufs_target.
+ * out[0] = loudness (LUFS), out[1] = 10 ** ((lufs_target - L) / 20). */
+int mm_op_loudness(mm_ctx *ctx, const mm_job *job, int dtype, const void *in, double *out);
+/* apply_multiband_compressor (AME:196-210) on int16 PCM [frames][channels]:
+ * job with multiband_on, in_kind MM_IN_I16, EQ/exciter/width/loudness off and one
+ * chunk covering the input (tile * tiles_per_chunk >= frames_proc); out has the
+ * input's frames (pydub overlay's ms re-slicing is the caller's). */
+int mm_op_multiband(mm_ctx *ctx, const mm_job *job, const int16_t *in, int16_t *out);
+
 /* ---- RCCL over xGMI ----------------------------------------------------- */
 int mm_comm_unique_id(char id_out[128]);
 int mm_comm_init(mm_ctx *ctx, int rank, int nranks, const char id[128]);

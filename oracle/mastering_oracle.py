@@ -207,8 +207,8 @@ def crossover_sos(rate, lo=250, hi=4000):
 BAND_TIMES = ((10.0, 200.0), (5.0, 150.0), (1.0, 50.0))  # (attack, release) ms, AME:207-209
 
 
-def band_split(q: np.ndarray, rate):
-    lp, hp = crossover_sos(rate)
+def band_split(q: np.ndarray, rate, crossover=(250, 4000)):
+    lp, hp = crossover_sos(rate, *crossover)
     x = pcm_to_float(q)
     lo = scipy.signal.sosfilt(lp, x, axis=0)
     hi = scipy.signal.sosfilt(hp, x, axis=0)
@@ -220,11 +220,31 @@ def overlay_add(a: np.ndarray, b: np.ndarray) -> np.ndarray:
     return np.clip(a.astype(np.int32) + b.astype(np.int32), -32768, 32767).astype(np.int16)
 
 
-def multiband(q: np.ndarray, rate, thresholds, ratios):
-    bands = band_split(q, rate)
+def multiband(q: np.ndarray, rate, thresholds, ratios, crossover=(250, 4000)):
+    bands = band_split(q, rate, crossover)
     outs = [compress_band(b, rate, t, r, at, rel)
             for b, t, r, (at, rel) in zip(bands, thresholds, ratios, BAND_TIMES)]
     return overlay_add(overlay_add(outs[0], outs[1]), outs[2])
+
+
+def overlay_length(frames: int, rate: int) -> int:
+    """Frames of `low.overlay(mid).overlay(high)` (AME:210): pydub's overlay
+    re-slices its first operand by ms, seg[0:len(seg)] (oracle/thirdparty_restated.py
+    AudioSegment.overlay / __getitem__), padding silence or dropping frames."""
+    n = int(round(1000 * (frames / rate)) * (rate / 1000.0))
+    return int(round(1000 * (n / rate)) * (rate / 1000.0))
+
+
+def apply_multiband_compressor(q: np.ndarray, rate, thresholds, ratios, crossover=(250, 4000)):
+    """AME:196-210 on one int16 chunk, with the overlay's length semantics."""
+    out = multiband(q, rate, thresholds, ratios, crossover)
+    n1 = overlay_length(q.shape[0], rate)
+    if n1 != q.shape[0]:
+        pad = np.zeros((n1,) + q.shape[1:], np.int16)
+        k = min(n1, q.shape[0])
+        pad[:k] = out[:k]
+        out = pad
+    return out
 
 
 def multiband_params(settings):

@@ -4,7 +4,10 @@
 #include <stdint.h>
 
 // Python float / numpy semantics: no implicit FMA contraction anywhere.  The
-// linear-recurrence kernels call fma() explicitly where it is wanted.
+// linear-recurrence kernels call fma() explicitly where it is wanted.  The pragma
+// covers code in these files; the Makefile also passes -ffp-contract=off, because
+// HIP's __fmul_rn/__fadd_rn bodies are compiled before it and were fused into
+// v_fma_f32 when inlined next to each other (seen in the f32 soft limiter).
 #pragma clang fp contract(off)
 
 namespace mm {
@@ -13,6 +16,11 @@ namespace mm {
 // every outstanding global access (vmcnt(0)), i.e. it stalls on the block's own
 // in-flight stores and drains register prefetch pipelines at every barrier.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Correctly rounded f32 square root (numpy's np.sqrt / x ** 0.5 on float32).
+// __fsqrt_rn lowers to v_sqrt_f32 (1 ulp) on gfx950; the f64 square root is
+// correctly rounded and rounding it to f32 is exact-safe (53 >= 2*24 + 2 bits).
+__device__ __forceinline__ float sqrt_f32_cr(float x) { return (float)__dsqrt_rn((double)x); }
 
 // Software-pipelined sequential stream over elements 0..len-1: ld(i) returns
 // element i and MUST be safe (clamped) for any i < len + NB*B; proc(v) consumes

@@ -44,7 +44,7 @@ __device__ __forceinline__ float limiter32(float y) {
     if (ay > 0.98f) {
         float d = __fsub_rn(ay, 0.98f);
         float t = __fdiv_rn(d, 0.02f);
-        float den = __fsqrt_rn(__fadd_rn(1.0f, __fmul_rn(t, t)));
+        float den = sqrt_f32_cr(__fadd_rn(1.0f, __fmul_rn(t, t)));
         float v = __fadd_rn(0.98f, __fdiv_rn(d, den));
         float sg = y > 0 ? 1.0f : (y < 0 ? -1.0f : y);
         y = __fmul_rn(v, sg);

@@ -1091,3 +1091,6 @@ int mm_allgather_f64(mm_ctx *c, const double *host_in, double *host_out, int64_t
 }
 
 }  // extern "C"
+
+// per-stage operators (AME:117-227 one at a time)
+#include "ops.hip"

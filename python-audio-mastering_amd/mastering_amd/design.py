@@ -26,6 +26,7 @@ import scipy.signal
 MAX_DIM = 8
 CHUNK_MS = 30 * 1000  # AME:48
 DEFAULT_TILE = 125     # divides 30 s chunks at every rate that is a multiple of 25 Hz
+OPS_TILE = 125         # tile of the per-stage operators' look-back tables (== OPS_TILE in csrc/ops.hip)
 
 EQ_KEYS = ("bass_boost", "mid_cut", "presence_boost", "treble_boost")
 BAND_TIMES = ((10.0, 200.0), (5.0, 150.0), (1.0, 50.0))  # (attack, release) ms, AME:207-209
@@ -58,6 +59,28 @@ def chunk_bounds(frames: int, rate: int):
             raise ValueError("TooManyMissingFrames")
         out.append((a, b))
     return out
+
+
+def check_chunk_geometry(bounds, nominal: int, rate: int, multiband: bool):
+    """The tile-major timeline needs every 30 s chunk but the last to hold exactly
+    `nominal` frames, and (with the multiband stage) pydub's overlay to keep each
+    chunk's length (AME:210 re-slices the low band by ms: `seg[0:len(seg)]`).
+
+    Both hold at every rate above 2 kHz: a chunk starts and ends at
+    int(ms * (rate / 1000.0)) for whole ms (AME:54), the same expression that the
+    overlay's re-slice evaluates after `len()` rounds the length back to the same
+    ms (the rounding error 1000 / rate < 0.5 ms), and the checked rates 8-192 kHz
+    give uniform chunks up to the 2^31-frame limit (tests/test_oracle.py).  Below
+    2 kHz the reference's slicing can drop or pad frames per chunk; the engine
+    refuses such input instead of mis-slicing it."""
+    for a, b in bounds[:-1]:
+        if b - a != nominal:
+            raise NotImplementedError(f"non-uniform 30 s chunk lengths at {rate} Hz")
+    if multiband:
+        for a, b in bounds:
+            f = b - a
+            if pydub_frame(pydub_len_ms(f, rate), rate) != f:
+                raise NotImplementedError(f"pydub overlay re-slicing changes a chunk's length at {rate} Hz")
 
 
 def choose_tile(chunk_frames: int, preferred: int = DEFAULT_TILE) -> int:
@@ -127,7 +150,10 @@ def eq_sections(rate, params):
     return secs
 
 
-def crossover_sections(rate, low_hz=250, high_hz=4000):
+LOW_CROSSOVER, HIGH_CROSSOVER = 250, 4000  # apply_multiband_compressor defaults (AME:196)
+
+
+def crossover_sections(rate, low_hz=LOW_CROSSOVER, high_hz=HIGH_CROSSOVER):
     """AME:197-198: butter(4) LP and HP as 2 SOS sections each."""
     lp = scipy.signal.butter(4, low_hz, btype="lowpass", fs=rate, output="sos")
     hp = scipy.signal.butter(4, high_hz, btype="highpass", fs=rate, output="sos")

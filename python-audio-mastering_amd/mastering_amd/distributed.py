@@ -162,12 +162,34 @@ class TorchCollectives:
         return t.cpu().numpy()
 
 
+def rccl_unique_id() -> bytes:
+    """A fresh RCCL unique id (128 bytes) for mm_comm_init; rank 0 makes it and
+    hands it to the other ranks out of band (bench.py: a gloo broadcast)."""
+    lib = native.load()
+    buf = ctypes.create_string_buffer(128)
+    rc = lib.mm_comm_unique_id(buf)
+    if rc != 0:
+        raise RuntimeError(f"mm_comm_unique_id failed ({rc})")
+    return buf.raw
+
+
 class LibraryCollectives:
     """The same two collectives through the library's own RCCL communicator
-    (mm_comm_init / mm_allgather_f64 / mm_allreduce_sum_f64)."""
+    (mm_comm_init / mm_allgather_f64 / mm_allreduce_sum_f64): one rank per GPU,
+    RCCL over xGMI between them."""
 
     def __init__(self, ctx: native.Context, world: int):
         self.ctx, self.world = ctx, world
+
+    @classmethod
+    def create(cls, ctx: native.Context, rank: int, world: int, unique_id: bytes) -> "LibraryCollectives":
+        if len(unique_id) != 128:
+            raise ValueError("RCCL unique id must be 128 bytes")
+        ctx.check(ctx.lib.mm_comm_init(ctx.ptr, int(rank), int(world), unique_id), "mm_comm_init")
+        return cls(ctx, world)
+
+    def close(self):
+        self.ctx.check(self.ctx.lib.mm_comm_destroy(self.ctx.ptr), "mm_comm_destroy")
 
     def all_gather(self, vec: np.ndarray) -> np.ndarray:
         v = np.ascontiguousarray(vec, dtype=np.float64)

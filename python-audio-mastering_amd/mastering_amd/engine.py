@@ -39,31 +39,33 @@ class Job:
     """A planned mastering job: the mm_job POD plus the host arrays it points to."""
 
     def __init__(self, frames_in: int, rate: int, channels: int, params: dict, out_kind: int = native.MM_OUT_I16,
-                 seg_bounds=None, check_length: bool = True):
+                 seg_bounds=None, check_length: bool = True, single_chunk: bool = False,
+                 crossover=(design.LOW_CROSSOVER, design.HIGH_CROSSOVER)):
         """`seg_bounds` (time-sharded ranks, distributed.py): this range's loudness
         segment bounds relative to its first frame; the whole-track gating then
         happens on the host after the all-reduce.  `check_length=False` skips
-        pyloudnorm's minimum-length check (it applies to the whole track)."""
+        pyloudnorm's minimum-length check (it applies to the whole track).
+        `single_chunk`: the whole input is ONE line (the per-stage operators of
+        ops.py, which the reference calls on one chunk) instead of AME:48's 30 s
+        chunks; `crossover`: apply_multiband_compressor's (low, high) Hz."""
         if channels not in (1, 2):
             raise ValueError("only mono and stereo are supported (AME:119,137,152)")
         params = dict(params or {})
         self.params = params
         self.rate, self.channels, self.frames_in = int(rate), int(channels), int(frames_in)
-        bounds = design.chunk_bounds(self.frames_in, self.rate)
+        multiband = bool(params.get("multiband"))
+        if single_chunk:
+            bounds = [(0, self.frames_in)] if self.frames_in else []
+            self.tile = design.OPS_TILE
+            self.tiles_per_chunk = max(1, -(-self.frames_in // self.tile))
+        else:
+            bounds = design.chunk_bounds(self.frames_in, self.rate)
+            nominal = design.pydub_frame(design.CHUNK_MS, self.rate)
+            design.check_chunk_geometry(bounds, nominal, self.rate, multiband)
+            self.tile = design.choose_tile(nominal)
+            self.tiles_per_chunk = nominal // self.tile
         self.chunks = bounds
         self.frames_proc = bounds[-1][1] if bounds else 0
-        nominal = design.pydub_frame(design.CHUNK_MS, self.rate)
-        for a, b in bounds[:-1]:
-            if b - a != nominal:
-                raise NotImplementedError("non-uniform 30 s chunk lengths at this rate")
-        self.tile = design.choose_tile(nominal)
-        self.tiles_per_chunk = nominal // self.tile
-        multiband = bool(params.get("multiband"))
-        if multiband:
-            for a, b in bounds:  # overlay's ms re-slicing must not change the chunk length (AME:210)
-                f = b - a
-                if design.pydub_frame(design.pydub_len_ms(f, self.rate), self.rate) != f:
-                    raise NotImplementedError("chunk length not preserved by pydub overlay slicing")
         lufs = params.get("lufs")
         if check_length and lufs is not None and self.frames_proc < 0.4 * self.rate:
             # pyloudnorm util.valid_audio (AME:218)
@@ -89,7 +91,7 @@ class Job:
         self._fill_iir(j.eq, eq, [len(eq)], self.tile, tpb)
         # --- crossover (2 branches of 2)
         if multiband:
-            self._fill_iir(j.xover, design.crossover_sections(self.rate), [2, 2], self.tile, tpb)
+            self._fill_iir(j.xover, design.crossover_sections(self.rate, *crossover), [2, 2], self.tile, tpb)
             self._tables = []
             for b in range(3):
                 tk, td, rk, rd = design.BAND_DEFAULTS[b]

@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get("MM_LIB") or os.path.join(_HERE, "libmastering_amd.so"
 
 MM_OUT_I16, MM_OUT_F32 = 0, 1
 MM_IN_F32, MM_IN_I16 = 0, 1
+MM_F32, MM_F64 = 0, 1  # per-stage operator sample dtypes
 MM_ERR_ARG = -1
 MAX_DIM, TILE_POW, BLK_POW = 8, 8, 65
 
@@ -65,7 +66,9 @@ class MMWavInfo(ctypes.Structure):
 EXPORTS = ("mm_create", "mm_destroy", "mm_last_error", "mm_sync", "mm_version", "mm_master", "mm_master_device",
            "mm_stage_chunks", "mm_kweight_range_end", "mm_hop_energies", "mm_gate_loudness", "mm_finalize",
            "mm_read_mix", "mm_timing", "mm_kernel_stats", "mm_comm_unique_id", "mm_comm_init", "mm_comm_destroy",
-           "mm_allreduce_sum_f64", "mm_allgather_f64", "mm_wav_probe", "mm_master_wav")
+           "mm_allreduce_sum_f64", "mm_allgather_f64", "mm_wav_probe", "mm_master_wav",
+           "mm_op_pcm_to_float", "mm_op_saturation", "mm_op_stereo_width", "mm_op_quantize", "mm_op_soft_limiter",
+           "mm_op_gain", "mm_op_sosfilt", "mm_op_loudness", "mm_op_multiband")
 
 _lib = None
 _lock = threading.Lock()
@@ -110,6 +113,16 @@ def load():
             "mm_comm_destroy": ([vp], ctypes.c_int),
             "mm_allreduce_sum_f64": ([vp, c_double_p, ctypes.c_int64], ctypes.c_int),
             "mm_allgather_f64": ([vp, c_double_p, c_double_p, ctypes.c_int64], ctypes.c_int),
+            "mm_op_pcm_to_float": ([vp, vp, ctypes.c_int64, vp], ctypes.c_int),
+            "mm_op_saturation": ([vp, ctypes.c_int, vp, ctypes.c_int64, ctypes.c_double, vp], ctypes.c_int),
+            "mm_op_stereo_width": ([vp, ctypes.c_int, vp, ctypes.c_int64, ctypes.c_double, vp], ctypes.c_int),
+            "mm_op_quantize": ([vp, ctypes.c_int, vp, ctypes.c_int64, vp], ctypes.c_int),
+            "mm_op_soft_limiter": ([vp, ctypes.c_int, vp, ctypes.c_int64, ctypes.c_double], ctypes.c_int),
+            "mm_op_gain": ([vp, ctypes.c_int, vp, ctypes.c_int64, ctypes.c_double, vp], ctypes.c_int),
+            "mm_op_sosfilt": ([vp, ctypes.c_int, vp, ctypes.c_int64, ctypes.c_int, P(MMIir), ctypes.c_int, vp],
+                              ctypes.c_int),
+            "mm_op_loudness": ([vp, P(MMJob), ctypes.c_int, vp, c_double_p], ctypes.c_int),
+            "mm_op_multiband": ([vp, P(MMJob), vp, vp], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             fn = getattr(lib, name)

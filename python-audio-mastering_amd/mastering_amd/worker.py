@@ -34,9 +34,17 @@ def object_path(uri: str, root: str | None = None) -> tuple[str, str, str]:
     bucket, blob = rest.split("/", 1)
     if not bucket or not blob or blob.endswith("/"):
         raise ValueError(f"not an object URI (gs://<bucket>/<blob>): {uri!r}")
+    # a bucket is one path component below the root: no '.', '..' or separators
+    if bucket in (".", "..") or os.sep in bucket or (os.altsep and os.altsep in bucket):
+        raise ValueError(f"bad bucket name in {uri!r}")
+    root_abs = os.path.abspath(root)
     bucket_dir = os.path.join(root, bucket)
+    bucket_abs = os.path.abspath(bucket_dir)
     path = os.path.normpath(os.path.join(bucket_dir, blob))
-    if os.path.commonpath([os.path.abspath(path), os.path.abspath(bucket_dir)]) != os.path.abspath(bucket_dir):
+    path_abs = os.path.abspath(path)
+    if os.path.commonpath([bucket_abs, root_abs]) != root_abs or bucket_abs == root_abs:
+        raise ValueError(f"bucket escapes the object root: {uri!r}")
+    if os.path.commonpath([path_abs, bucket_abs]) != bucket_abs or path_abs == bucket_abs:
         raise ValueError(f"object name escapes its bucket: {uri!r}")
     return path, bucket_dir, blob
 

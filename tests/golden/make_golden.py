@@ -182,6 +182,30 @@ def primitives(ame):
     edge = np.array([1.0, 32767.9 / 32768, -1.0, -0.7 / 32768, np.nan, 1.5, -2.0, 0.49999], np.float64)
     d["prim_quant_in"] = edge
     d["prim_quant_out"] = np.frombuffer(ame.float_array_to_audio_segment(edge, _Seg()), np.int16)
+    # apply_multiband_compressor (AME:196-210) on pydub segments: 2.5 s stereo with
+    # thresholds where every branch fires, a ragged 8192-frame chunk (overlay pads it
+    # to 186 ms = 8202 frames) and mono at 48 kHz with custom crossovers
+    mb = [("prim_mb_hot", pink_noise_pcm16(110250, sr, 2, 21), sr, (-16.0, 6.0, -21.0, 3.0, -27.0, 4.0), {}),
+          ("prim_mb_ragged", q, sr, (-25.0, 6.0, -20.0, 3.0, -15.0, 4.0), {}),
+          ("prim_mb_mono48k", pink_noise_pcm16(72000, 48000, 1, 22), 48000, (-18.0, 4.0, -24.0, 2.0, -30.0, 8.0),
+           {"low_crossover": 300, "high_crossover": 5000})]
+    for name, pcm, rate, args, kw in mb:
+        ch = 1 if pcm.ndim == 1 else 2
+        seg = tp.AudioSegment(np.ascontiguousarray(pcm, dtype="<i2").tobytes(), 2, rate, ch)
+        out = ame.apply_multiband_compressor(seg, *args, **kw)
+        o = np.frombuffer(out._data, np.int16)
+        d[f"{name}_in"] = pcm
+        d[f"{name}_out"] = o.reshape(-1, 2) if ch == 2 else o
+        d[f"{name}_args"] = np.array(list(args) + [kw.get("low_crossover", 250), kw.get("high_crossover", 4000), rate],
+                                     np.float64)
+    # normalize_to_lufs (AME:212-222): f32 stereo (f64 out) and f64 mono
+    for name, x, rate, target in [("prim_norm_f32", pink_noise_pcm16(3 * sr, sr, 2, 23).astype(np.float32) / 32768,
+                                   sr, -14.0),
+                                  ("prim_norm_f64_mono", rng.standard_normal(2 * 48000) * 0.05, 48000, -16.0)]:
+        _LOUDNESS.clear()
+        d[f"{name}_in"] = x
+        d[f"{name}_out"] = ame.normalize_to_lufs(x.copy(), rate, target)
+        d[f"{name}_meta"] = np.array([rate, target, _LOUDNESS[-1]], np.float64)
     return d
 
 
@@ -189,6 +213,9 @@ def main():
     ame = load_reference()
     meta = {}
     only = set(sys.argv[1:])
+    if only == {"primitives"}:  # per-stage vectors only
+        np.savez_compressed(os.path.join(HERE, "primitives.npz"), **primitives(ame))
+        return
     for name, pcm, rate, st in cases():
         if only and name not in only:
             continue

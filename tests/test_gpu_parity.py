@@ -35,12 +35,13 @@ def _check(out, info, ref, L):
     return r, exact
 
 
-@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "*.npz"))))
+GOLDEN_CASES = sorted(p for p in glob.glob(os.path.join(GOLDEN, "*.npz")) if not p.endswith("primitives.npz"))
+
+
+@pytest.mark.parametrize("path", GOLDEN_CASES, ids=[os.path.basename(p)[:-4] for p in GOLDEN_CASES])
 def test_golden(path):
+    """Every reference golden through master_pcm (per-stage vectors: test_ops.py)."""
     from mastering_amd import master_pcm
-    name = os.path.basename(path)
-    if name == "primitives.npz":
-        pytest.skip("per-stage vectors are checked on CPU")
     d = np.load(path)
     st = json.loads(str(d["settings"]))
     out, info = master_pcm(d["pcm"], int(d["rate"]), st)

@@ -1,7 +1,7 @@
 """GUI engine API (mastering_amd.gui_compat): process_audio / batch_process_audio as
 mastering_gui.py:192-232 calls them.  CPU tests swap engine.process for a recorder;
-the GPU test masters real WAV files through the C-ABI and checks them against
-master_pcm."""
+the GPU tests master reference goldens as WAV files through the C-ABI and check
+them against the reference's own outputs."""
 import os
 
 import numpy as np
@@ -90,24 +90,51 @@ def test_batch_shards_files_over_devices(tmp_path, fake_engine):
     assert sum(m.startswith("Processed") for m in msgs) == len(names)
 
 
+P_HOT_GUI = {  # tests/golden P_HOT in the GUI's keys (mastering_gui.py:181-190)
+    "bass_boost": 4.0, "mid_cut": 3.0, "presence_boost": 1.0, "treble_boost": 3.0, "saturation": 30, "width": 1.3,
+    "multiband": True, "lufs": -14.0, "compress": False, "low_band_threshold": -16.0, "mid_band_threshold": -21.0,
+    "high_band_threshold": -27.0,
+}
+
+
 @pytest.mark.gpu
-def test_batch_on_gpu_matches_master_pcm(tmp_path):
-    from mastering_amd import gui_compat, master_pcm, wavio
-    from mastering_amd.synth import pink_noise_pcm16
+def test_batch_on_gpu_matches_reference_goldens(tmp_path):
+    """batch_process_audio over reference goldens that share one settings dict (P_HOT
+    via the GUI's band keys): every output file holds the reference's own output."""
+    import json
+
+    from conftest import GOLDEN
+    from mastering_amd import gui_compat, wavio
+    from test_wav_path import check_against_golden
     src = tmp_path / "in"
     src.mkdir()
-    pcms = {}
-    for i, secs in enumerate((3, 5)):
-        pcm = pink_noise_pcm16(secs * 44100, 44100, 2, 20 + i)
-        name = f"clip{i}.wav"
-        wavio.write_wav(str(src / name), pcm, 44100)
-        pcms[name] = pcm
+    golden = {}
+    for name in ("hot_4s", "mono_hot_2s", "hot_96k_1s"):
+        d = np.load(os.path.join(GOLDEN, name + ".npz"))
+        assert json.loads(str(d["settings"])) == gui_compat.chain_settings({k: v for k, v in P_HOT_GUI.items()})
+        wavio.write_wav(str(src / f"{name}.wav"), d["pcm"], int(d["rate"]))
+        golden[f"{name}.wav"] = d
     msgs = []
-    res = gui_compat.batch_process_audio(GUI_SETTINGS, str(src), str(tmp_path / "out"), msgs.append)
+    res = gui_compat.batch_process_audio(P_HOT_GUI, str(src), str(tmp_path / "out"), msgs.append)
     assert "complete" in msgs[-1].lower() and "error" not in msgs[-1].lower()
-    params = gui_compat.chain_settings(GUI_SETTINGS)
-    for name, pcm in pcms.items():
+    for name, d in golden.items():
         got, rate = wavio.read_wav(str(tmp_path / "out" / gui_compat.output_name(name)))
-        ref, info = master_pcm(pcm, 44100, params)
-        assert rate == 44100 and np.array_equal(got, ref)
-        assert abs(res[name]["loudness"] - info["loudness"]) < 1e-9
+        assert rate == int(d["rate"])
+        check_against_golden(got, res[name], d["out"], float(d["loudness"]))
+
+
+@pytest.mark.gpu
+def test_process_audio_on_gpu_matches_reference_golden(tmp_path):
+    from conftest import GOLDEN
+    from mastering_amd import gui_compat, wavio
+    from test_wav_path import check_against_golden
+    d = np.load(os.path.join(GOLDEN, "full_4s.npz"))
+    wavio.write_wav(str(tmp_path / "a.wav"), d["pcm"], int(d["rate"]))
+    s = {"bass_boost": 4.0, "mid_cut": 3.0, "presence_boost": 1.0, "treble_boost": 3.0, "saturation": 30,
+         "width": 1.3, "multiband": True, "lufs": -14.0, "input_file": str(tmp_path / "a.wav"),
+         "output_file": str(tmp_path / "b.wav")}
+    msgs = []
+    info = gui_compat.process_audio(s, msgs.append)
+    assert "complete" in msgs[-1].lower()
+    got, _ = wavio.read_wav(str(tmp_path / "b.wav"))
+    check_against_golden(got, info, d["out"], float(d["loudness"]))

@@ -1,0 +1,175 @@
+"""The per-stage operator surface (mastering_amd.ops, the reference's AME:117-227
+helpers one at a time).  CPU: the identity / pass-through paths that never reach
+the library, and argument checks.  GPU (through the C-ABI's mm_op_* entry
+points): every vector of tests/golden/primitives.npz, which the reference's OWN
+helpers produced (tests/golden/make_golden.py), within the tolerance written on
+each check.
+
+Tolerances: integer outputs (quantise, multiband int16) bit-exact except where a
+floating-point stage before a truncation can land on the other side of an
+integer (stated per test); f64 IIR outputs 1e-12 absolute (the look-back composes
+tile carries in a different order than scipy's sequential loop); f32 tanh 2 ulp
+(numpy's f32 tanh is not correctly rounded); everything else bit-exact."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+
+@pytest.fixture(scope="module")
+def prim():
+    return np.load(os.path.join(GOLDEN, "primitives.npz"))
+
+
+# ----------------------------------------------------------------- CPU
+def test_identity_paths_do_not_copy():
+    from mastering_amd import ops
+    x = np.zeros((16, 2), np.float32)
+    assert ops.apply_saturation(x, 0) is x  # AME:129
+    m = np.zeros(16, np.float32)
+    assert ops.apply_stereo_width(m, 1.5) is m  # AME:137
+    assert ops.apply_eq_to_samples(m, 44100, {}) is m
+    assert ops.apply_shelf_filter(m, 44100, 250, 0, "low") is m  # AME:171
+    assert ops.apply_peak_filter(m, 44100, 1000, 0) is m  # AME:186
+    y = ops.apply_eq_to_samples(x, 44100, {"bass_boost": 0.0})
+    assert y is not x and y.dtype == np.float32 and np.array_equal(y, x)
+
+
+def test_argument_checks():
+    from mastering_amd import ops
+    with pytest.raises(TypeError):
+        ops.apply_saturation(np.zeros(4, np.int16), 30)
+    with pytest.raises(ValueError):  # pyloudnorm valid_audio: shorter than one 0.4 s block
+        ops.normalize_to_lufs(np.zeros((1000, 2), np.float32), 44100)
+
+    class Seg24:
+        sample_width, channels, frame_rate = 3, 2, 44100
+    with pytest.raises(ValueError):
+        ops.audio_segment_to_float_array(Seg24())
+
+
+# ----------------------------------------------------------------- GPU
+class _Seg:
+    """pydub-AudioSegment-like (the attributes AME's helpers touch)."""
+
+    def __init__(self, data, channels, rate):
+        self._data, self.channels, self.frame_rate, self.sample_width = data, channels, rate, 2
+
+    def get_array_of_samples(self):
+        import array
+        return array.array("h", self._data)
+
+    def _spawn(self, data):
+        return _Seg(bytes(data), self.channels, self.frame_rate)
+
+
+@pytest.mark.gpu
+def test_pcm_conversions(prim):
+    from mastering_amd import ops
+    q = prim["prim_q"]
+    x = ops.audio_segment_to_float_array(_Seg(q.tobytes(), 2, 44100))
+    assert x.dtype == np.float32 and x.shape == q.shape and np.array_equal(x, q.astype(np.float32) / 32768)
+    with np.errstate(invalid="ignore"):
+        out = ops.float_array_to_audio_segment(prim["prim_quant_in"], _Seg(b"", 1, 44100))
+    assert np.array_equal(np.frombuffer(out._data, np.int16), prim["prim_quant_out"])  # bit-exact
+
+
+@pytest.mark.gpu
+def test_saturation(prim):
+    from mastering_amd import ops
+    x = prim["prim_q"].astype(np.float32) / 32768
+    for got_in, pct, key in [(x, 30, "prim_sat30"), (x * np.float32(3.0), 100, "prim_sat100")]:
+        y = ops.apply_saturation(got_in, pct)
+        ref = prim[key]
+        assert y.dtype == ref.dtype == np.float32
+        ulp = np.spacing(np.abs(ref).astype(np.float32))
+        assert np.all(np.abs(y - ref) <= 2 * ulp), np.max(np.abs(y - ref) / ulp)  # tanh: 2 ulp
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,preset,rate", [("techno", "techno", 44100), ("rock", "rock", 44100),
+                                              ("96k_dubstep", "dubstep", 96000)])
+def test_eq(prim, name, preset, rate):
+    from mastering_amd import EQ_PRESETS, ops
+    x = prim["prim_q"].astype(np.float32) / 32768
+    y = ops.apply_eq_to_samples(x, rate, EQ_PRESETS[preset])
+    ref = prim[f"prim_eq_{name}"]
+    assert y.dtype == ref.dtype == np.float64 and y.shape == ref.shape
+    assert np.max(np.abs(y - ref)) <= 1e-12
+
+
+@pytest.mark.gpu
+def test_shelf_and_peak_match_scipy(prim):
+    """apply_shelf_filter / apply_peak_filter per channel == the reference's per-stage
+    sosfilt chain (prim_eq_techno is their composition on each channel)."""
+    from mastering_amd import EQ_PRESETS, ops
+    st = EQ_PRESETS["techno"]
+    x = prim["prim_q"].astype(np.float32) / 32768
+    for c in range(2):
+        y = ops.apply_shelf_filter(x[:, c], 44100, 250, st["bass_boost"], "low")
+        y = ops.apply_peak_filter(y, 44100, 1000, -st["mid_cut"])
+        y = ops.apply_peak_filter(y, 44100, 4000, st["presence_boost"])
+        y = ops.apply_shelf_filter(y, 44100, 8000, st["treble_boost"], "high")
+        assert y.dtype == np.float64 and np.max(np.abs(y - prim["prim_eq_techno"][:, c])) <= 1e-12
+
+
+@pytest.mark.gpu
+def test_width(prim):
+    from mastering_amd import ops
+    x = prim["prim_q"].astype(np.float32) / 32768
+    y64 = ops.apply_stereo_width(x.astype(np.float64), 1.3)
+    y32 = ops.apply_stereo_width(x, 0.7)
+    assert y64.dtype == np.float64 and np.array_equal(y64, prim["prim_width13_f64"])  # bit-exact
+    assert y32.dtype == np.float32 and np.array_equal(y32, prim["prim_width07_f32"])
+
+
+@pytest.mark.gpu
+def test_soft_limiter(prim):
+    from mastering_amd import ops
+    x64 = prim["prim_lim_in"].copy()
+    x32 = prim["prim_lim_in"].astype(np.float32)
+    assert ops.soft_limiter(x64) is x64 and np.array_equal(x64, prim["prim_lim_out_f64"])  # in place, bit-exact
+    assert ops.soft_limiter(x32) is x32 and np.array_equal(x32, prim["prim_lim_out_f32"])
+    strided = np.repeat(prim["prim_lim_in"][:, None], 2, axis=1)[:, 0]  # non-contiguous view
+    ops.soft_limiter(strided)
+    assert np.array_equal(strided, prim["prim_lim_out_f64"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["prim_mb_hot", "prim_mb_ragged", "prim_mb_mono48k"])
+def test_multiband(prim, name):
+    """int16 out of the crossover + pydub compressor + overlay.  The crossover's f64
+    look-back carries may move a band sample across an int16 truncation boundary
+    (never seen on these vectors); the bar is >= 99.999 % identical samples and RMS
+    <= 1e-5, with the overlay's padded length exact."""
+    from mastering_amd import ops
+    a = prim[f"{name}_args"]
+    pcm, ref = prim[f"{name}_in"], prim[f"{name}_out"]
+    ch = 1 if pcm.ndim == 1 else 2
+    seg = ops.apply_multiband_compressor(_Seg(pcm.tobytes(), ch, int(a[8])), a[0], a[1], a[2], a[3], a[4], a[5],
+                                         low_crossover=a[6], high_crossover=a[7])
+    got = np.frombuffer(seg._data, np.int16)
+    got = got.reshape(-1, 2) if ch == 2 else got
+    arr = ops.apply_multiband_compressor(pcm, *a[:6], low_crossover=a[6], high_crossover=a[7], frame_rate=int(a[8]))
+    assert np.array_equal(arr, got)
+    assert got.shape == ref.shape
+    assert np.mean(got == ref) >= 0.99999, np.mean(got == ref)
+    assert np.sqrt(np.mean(((got.astype(np.float64) - ref) / 32768) ** 2)) <= 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["prim_norm_f32", "prim_norm_f64_mono"])
+def test_normalize_to_lufs(prim, name):
+    """Loudness within the north star's 0.1 LU and the internal 4e-4 LU; the output
+    (f64, = samples * np.float64 gain) then differs only by that gain ratio."""
+    from mastering_amd import ops
+    rate, target, L = prim[f"{name}_meta"]
+    x = prim[f"{name}_in"]
+    Lg = ops.integrated_loudness(x if x.ndim == 1 else x.mean(axis=1), int(rate))
+    assert abs(Lg - L) <= 4e-4
+    y = ops.normalize_to_lufs(x, int(rate), target)
+    ref = prim[f"{name}_out"]
+    assert y.dtype == ref.dtype == np.float64 and y.shape == ref.shape
+    assert np.max(np.abs(y - ref)) <= 1e-4 * np.max(np.abs(ref))

@@ -53,6 +53,26 @@ def test_primitives(oracle):
         assert np.array_equal(oracle.quantize(d["prim_quant_in"]), d["prim_quant_out"])
 
 
+@pytest.mark.parametrize("name", ["prim_mb_hot", "prim_mb_ragged", "prim_mb_mono48k"])
+def test_primitive_multiband(oracle, name):
+    """apply_multiband_compressor vectors from the reference's own AME:196-210
+    (overlay length semantics included: the ragged 8192-frame chunk comes back as
+    8202 frames)."""
+    d = np.load(os.path.join(GOLDEN, "primitives.npz"))
+    a = d[f"{name}_args"]
+    got = oracle.apply_multiband_compressor(d[f"{name}_in"], int(a[8]), (a[0], a[2], a[4]), (a[1], a[3], a[5]),
+                                            (a[6], a[7]))
+    assert got.shape == d[f"{name}_out"].shape and np.array_equal(got, d[f"{name}_out"])
+
+
+@pytest.mark.parametrize("name", ["prim_norm_f32", "prim_norm_f64_mono"])
+def test_primitive_normalize(oracle, name):
+    d = np.load(os.path.join(GOLDEN, "primitives.npz"))
+    rate, target, L = d[f"{name}_meta"]
+    got, Lo = oracle.normalize_to_lufs(d[f"{name}_in"], int(rate), target)
+    assert Lo == L and got.dtype == np.float64 and np.array_equal(got, d[f"{name}_out"])
+
+
 def test_quantize_kat(oracle):
     # SURVEY §8c: truncation, +1.0 wraps to -32768, NaN -> 0
     with np.errstate(invalid="ignore"):

@@ -1,12 +1,17 @@
 """The WAV file path of the C-ABI (mm_wav_probe / mm_master_wav):
 RIFF parsing against mastering_amd.wavio on the CPU (no GPU needed: a NULL context),
-and on the GPU the streamed file path against master_pcm on the decoded samples."""
+and on the GPU every reference golden pushed through process() as a WAV file and
+compared with the reference's own exported output (AME:43-98 end to end)."""
 import ctypes
+import glob
+import json
 import os
 import struct
 
 import numpy as np
 import pytest
+
+from conftest import GOLDEN
 
 
 def _probe(path):
@@ -79,38 +84,73 @@ def test_probe_rejects_bad_files(tmp_path):
     assert rc == 0 and info.frames == 98
 
 
+GOLDEN_CASES = sorted(p for p in glob.glob(os.path.join(GOLDEN, "*.npz")) if not p.endswith("primitives.npz"))
+
+
+def _golden(path):
+    d = np.load(path)
+    return d["pcm"], int(d["rate"]), json.loads(str(d["settings"])), d["out"], float(d["loudness"])
+
+
+def check_against_golden(got, info, ref, L):
+    """north_star tolerances: PCM RMS <= 1e-5 (decoded /32768), |dL| <= 0.1 LU; internal
+    loudness bar 4e-4 LU."""
+    assert got.shape == ref.shape and got.dtype == np.int16
+    rms = float(np.sqrt(np.mean(((got.astype(np.float64) - ref) / 32768.0) ** 2))) if ref.size else 0.0
+    assert rms <= 1e-5, rms
+    if np.isfinite(L):
+        assert abs(info["loudness"] - L) <= 4e-4
+    return rms
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind,ch,out_fmt", [("pcm16", 2, "pcm16"), ("pcm16", 1, "pcm16"), ("f32", 2, "f32")])
-def test_master_wav_matches_master_pcm(tmp_path, kind, ch, out_fmt):
-    from mastering_amd import master_pcm, process, wavio
-    from mastering_amd.synth import pink_noise_pcm16
-    P = {"bass_boost": 2.0, "saturation": 20, "width": 1.2, "multiband": True, "lufs": -14.0}
-    pcm = pink_noise_pcm16(7 * 44100 + 333, 44100, 2, 4)  # ragged length
-    if ch == 1:
-        pcm = np.ascontiguousarray(pcm[:, 0])
-    x = pcm if kind == "pcm16" else (pcm.astype(np.float32) / 32768)
+@pytest.mark.parametrize("path", GOLDEN_CASES, ids=[os.path.basename(p)[:-4] for p in GOLDEN_CASES])
+def test_process_wav_matches_reference_golden(tmp_path, path):
+    """AME:43 decode -> chain -> AME:98 export, end to end through files: the golden
+    input written as the PCM16 WAV the reference decoded, process() -> the output
+    WAV against the reference's own exported samples and measured loudness."""
+    from mastering_amd import process, wavio
+    pcm, rate, settings, ref, L = _golden(path)
     src, dst = tmp_path / "in.wav", tmp_path / "out.wav"
-    wavio.write_wav(str(src), x, 44100)
-    info = process(str(src), str(dst), dict(P, output_format=out_fmt))
-    got, rate = wavio.read_wav(str(dst))
-    ref, rinfo = master_pcm(x, 44100, P, out_kind=1 if out_fmt == "f32" else 0)
-    assert rate == 44100 and got.dtype == ref.dtype and np.array_equal(got, ref)
-    assert info["loudness"] == rinfo["loudness"]
+    wavio.write_wav(str(src), pcm, rate)
+    info = process(str(src), str(dst), settings)
+    got, r2 = wavio.read_wav(str(dst))
+    assert r2 == rate
+    check_against_golden(got, info, ref, L)
 
 
 @pytest.mark.gpu
-def test_master_wav_streams_large_files(tmp_path):
-    """70 s stereo PCM16 = 12 MB: crosses the 8 MB staging buffers in both directions."""
-    from mastering_amd import master_pcm, process, wavio
+@pytest.mark.parametrize("name", ["full_4s", "mono_hot_2s", "ragged_hot"])
+def test_process_float_wav_and_float_output(tmp_path, name):
+    """A 32-bit float WAV holding the same samples (PCM16 / 32768) masters to the same
+    result, and output_format='f32' writes that result / 32768.  (The reference would
+    decode a float WAV through ffmpeg as pcm_s32le with sample_width 4, which AME:121,
+    125 mis-scale: DESIGN.md §2 documents this deliberate deviation.)"""
+    from mastering_amd import process, wavio
+    pcm, rate, settings, ref, L = _golden(os.path.join(GOLDEN, name + ".npz"))
+    src, dst = tmp_path / "in.wav", tmp_path / "out.wav"
+    wavio.write_wav(str(src), pcm.astype(np.float32) / 32768, rate)
+    info = process(str(src), str(dst), dict(settings, output_format="f32"))
+    got, _ = wavio.read_wav(str(dst))
+    assert got.dtype == np.float32
+    assert np.array_equal(got * 32768, np.round(got * 32768))  # on the int16 grid
+    check_against_golden((got * 32768).astype(np.int16), info, ref, L)
+
+
+@pytest.mark.gpu
+def test_master_wav_streams_large_files(tmp_path, oracle):
+    """70 s stereo PCM16 = 12 MB: crosses the 8 MB staging buffers in both directions;
+    the file result against the oracle on the same samples."""
+    from mastering_amd import process, wavio
     from mastering_amd.synth import pink_noise_pcm16
     P = {"saturation": 10, "multiband": True, "lufs": -16.0}
     pcm = pink_noise_pcm16(70 * 44100, 44100, 2, 8)
     src, dst = tmp_path / "in.wav", tmp_path / "out.wav"
     wavio.write_wav(str(src), pcm, 44100)
-    process(str(src), str(dst), P)
+    info = process(str(src), str(dst), P)
     got, _ = wavio.read_wav(str(dst))
-    ref, _ = master_pcm(pcm, 44100, P)
-    assert np.array_equal(got, ref)
+    ref, L = oracle.master(pcm, 44100, P, return_loudness=True)
+    check_against_golden(got, info, ref, L)
 
 
 @pytest.mark.gpu

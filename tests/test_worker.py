@@ -1,7 +1,7 @@
 """Worker adapter (mastering_amd.worker): the Pub/Sub push handler of
 worker/main.py:15-50 and the object-store flow of AME:24-113 on a local tree.
-CPU tests swap engine.process for a recorder; the GPU test masters a real object
-and checks it against master_pcm."""
+CPU tests swap engine.process for a recorder; the GPU test masters reference
+goldens as objects and checks them against the reference's own outputs."""
 import base64
 import io
 import json
@@ -37,7 +37,8 @@ def test_object_path(tmp_path):
     p, bdir, blob = object_path("gs://bkt/uploads/a.wav", str(tmp_path))
     assert p == str(tmp_path / "bkt" / "uploads" / "a.wav") and bdir == str(tmp_path / "bkt")
     assert blob == "uploads/a.wav"
-    for bad in ("gs://bkt", "gs://bkt/", "gs:///x.wav", "gs://bkt/../other/x.wav"):
+    for bad in ("gs://bkt", "gs://bkt/", "gs:///x.wav", "gs://bkt/../other/x.wav", "gs://../x.wav",
+                "gs://./x.wav", "gs://bkt/./", "gs://bkt/sub/../../x.wav"):
         with pytest.raises(ValueError):
             object_path(bad, str(tmp_path))
 
@@ -99,16 +100,25 @@ def test_wsgi_app(tmp_path, fake_engine, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_worker_job_on_gpu(tmp_path):
-    from mastering_amd import master_pcm, wavio
-    from mastering_amd.synth import pink_noise_pcm16
+@pytest.mark.parametrize("name", ["full_4s", "hot_4s", "nolufs_dubstep_3s"])
+def test_worker_job_on_gpu(tmp_path, name):
+    """A push job on a reference golden: the object written under processed/ holds the
+    reference's own output (AME:24-113 end to end, worker/main.py:15-50)."""
+    import json as _json
+
+    from conftest import GOLDEN
+    from mastering_amd import wavio
     from mastering_amd.worker import handle_push
-    pcm = pink_noise_pcm16(4 * 44100, 44100, 2, 31)
-    (tmp_path / "bkt").mkdir()
-    wavio.write_wav(str(tmp_path / "bkt" / "track.wav"), pcm, 44100)
-    settings = {"saturation": 30, "width": 1.3, "multiband": True, "lufs": -14.0, "bass_boost": 3}
-    assert handle_push(_envelope({"gcs_uri": "gs://bkt/track.wav", "settings": settings}), str(tmp_path)) == ("", 204)
+    from test_wav_path import check_against_golden
+    d = np.load(os.path.join(GOLDEN, name + ".npz"))
+    settings = _json.loads(str(d["settings"]))
+    (tmp_path / "bkt" / "uploads").mkdir(parents=True)
+    wavio.write_wav(str(tmp_path / "bkt" / "uploads" / "track.wav"), d["pcm"], int(d["rate"]))
+    env = _envelope({"gcs_uri": "gs://bkt/uploads/track.wav", "settings": settings})
+    assert handle_push(env, str(tmp_path)) == ("", 204)
     got, rate = wavio.read_wav(str(tmp_path / "bkt" / "processed" / "mastered_track.wav"))
-    ref, _ = master_pcm(pcm, 44100, settings)
-    assert rate == 44100 and np.array_equal(got, ref)
+    assert rate == int(d["rate"])
+    from mastering_amd import process
+    info = process(str(tmp_path / "bkt" / "uploads" / "track.wav"), str(tmp_path / "again.wav"), settings)
+    check_against_golden(got, info, d["out"], float(d["loudness"]))
     assert (tmp_path / "bkt" / "processed" / "mastered_track.wav.complete").exists()
