@@ -1,32 +1,50 @@
 """Benchmark: stereo frames/s through the full mastering chain (BASELINE.json metric).
 
-Workload at N=1 is BASELINE config C2: one 5-min 44.1 kHz stereo f32 track, full
-chain (exciter 30 %, techno EQ, width 1.3, 3-band compressor with the worker's
-default thresholds, LUFS -14) on one MI355X.  For N>1 every rank masters its own
-5-min track (file sharding as in C3: no data-path collective) -> "scaling": "weak".
-A "step" = one complete mastering of the track with input and output resident
-in HBM (mm_master_device: every kernel of the chain plus its single host sync).
+Workloads (`--workload`, BASELINE.json configs; a "step" masters every track of
+the rank's share once, inputs and outputs resident in HBM):
+  C2  one 5-min 44.1 kHz stereo f32 track per GPU (default; BASELINE's 1-GPU
+      config).  With N > 1 every rank masters its own track: file sharding, no
+      data-path collective, "scaling": "weak".
+  C3  8 x 3-min 44.1 kHz tracks per GPU (64 tracks over 8 GPUs), file-sharded,
+      run as one mm_master_batch (up to 8 tracks in flight on their own streams).
+  C4  one 2-h 44.1 kHz track time-sharded over the N ranks: each rank stages its
+      contiguous 30 s chunks, then the K-weighting carry all-gather and ONE sum
+      all-reduce of the 0.1 s loudness energies run through the library's own RCCL
+      communicator (mm_comm_init; RCCL over xGMI), "scaling": "strong".
+  C5  16 x 3-min 96 kHz f32 tracks per GPU (128 over 8 GPUs), f32 out, batched.
+Full chain settings P_FULL (exciter 30 %, techno EQ, width 1.3, 3-band compressor
+with the worker's default thresholds, LUFS -14); `--params hot` switches to the
+P_HOT thresholds (every compressor branch fires: the envelope solve's worst case
+measured here).
 
 Timing: W warm-up steps, then K steps timed with no instrumentation, bracketed
-by a barrier + device sync on both sides (max over ranks).  A separate profiling
-pass (HIP events around every launch on the library's stream) gives per-kernel
-device times; the dominant kernel's roofline uses its ALGORITHMIC bytes per
-launch over its average launch duration.  `traffic` comes from the
-committed rocprofv3 PMC summary of the same command (tools/pmc.sh ->
-profiles/<round>_pmc_summary.json) when present.
+by a barrier + device sync on both sides (max over ranks).  A separate pass with
+HIP events around every launch on the library's streams gives per-kernel device
+times.  roofline: the chain's algorithmic bytes (16 B per stereo frame: f32 L,R
+in + f32 L,R out) over ms_per_step is the headline; the dominant
+kernel's own algorithmic bytes per launch over its event-timed average launch sit
+beside it.  `traffic` = PMC bytes per step from profiles/<tag>_pmc_summary.json,
+used only when that profile was measured on these exact kernel sources (its
+source_sha matches).  `limiter` comes from the SQ issue/wait shares recorded next
+to it.  cpu_baseline: the faithful-cost CPU path (oracle/faithful_cost.py: the
+reference's numpy/scipy stages + pydub's per-frame Python compressor loop) on
+whole chunks, extrapolated, on 1 core and on the box's cores; it runs before
+anything touches the GPU (its worker processes are forked).
 
-Run:  python bench.py [--gpus N] [--steps K] [--warmup W]
+Run:  python bench.py [--workload C2|C3|C4|C5] [--gpus N] [--steps K] [--warmup W]
 Multi-GPU (driver): python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
 
 import argparse
+import glob
+import hashlib
 import json
 import os
 import sys
 import time
 
-os.environ.setdefault("OMP_NUM_THREADS", "1")  # CPU baseline leg: one core
+os.environ.setdefault("OMP_NUM_THREADS", "1")  # CPU baseline leg: one core per process
 os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")
 os.environ.setdefault("MKL_NUM_THREADS", "1")
 
@@ -38,15 +56,35 @@ import numpy as np  # noqa: E402
 
 METRIC = "stereo frames/sec through full mastering chain, 44.1 kHz f32; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_summary.json")
+CHAIN_BYTES_PER_FRAME = 16  # f32 L,R in + f32 L,R out
 P_FULL = {"bass_boost": 4.0, "mid_cut": 3.0, "presence_boost": 1.0, "treble_boost": 3.0,
           "saturation": 30, "width": 1.3, "multiband": True, "lufs": -14.0}
+P_HOT = dict(P_FULL, low_thresh=-16.0, mid_thresh=-21.0, high_thresh=-27.0)
+WORKLOADS = {
+    "C2": {"rate": 44100, "seconds": 300, "tracks": 1, "desc": "C2: 5-min 44.1 kHz stereo f32 track per GPU"},
+    "C3": {"rate": 44100, "seconds": 180, "tracks": 8, "desc": "C3: 8 x 3-min 44.1 kHz stereo f32 tracks per GPU "
+                                                             "(64 over 8 GPUs), file-sharded, batched"},
+    "C4": {"rate": 44100, "seconds": 7200, "tracks": 1, "desc": "C4: one 2-h 44.1 kHz stereo f32 track time-sharded "
+                                                              "over the ranks, RCCL carry all-gather + energy "
+                                                              "all-reduce"},
+    "C5": {"rate": 96000, "seconds": 180, "tracks": 16, "desc": "C5: 16 x 3-min 96 kHz stereo f32 tracks per GPU "
+                                                              "(128 over 8 GPUs), f32 hi-res out, batched"},
+}
 
 
-ENVELOPE_NOTE = ("the compressor envelope is a sequential non-linear recurrence solved exactly by speculative "
-                 "super-tile walks (one lane each, ~0.4 waves per SIMD): VALU-issue and dependent-latency bound, "
-                 "not HBM bound; the warm-up re-reads each M from the memory fabric ~7x (PMC traffic) "
-                 "(DESIGN.md §4)")
+def source_sha() -> str:
+    """Hash of everything that shapes the kernels' work (HIP sources, header, host
+    geometry): a profile under profiles/ is used only for the exact same code."""
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "python-audio-mastering_amd", "csrc", "*")))
+    files += [os.path.join(ROOT, "include", "mastering.h"),
+              os.path.join(ROOT, "python-audio-mastering_amd", "mastering_amd", "engine.py"),
+              os.path.join(ROOT, "python-audio-mastering_amd", "mastering_amd", "design.py")]
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def algorithmic_bytes(kernel, n, g, active, walked_per_launch):
@@ -77,37 +115,134 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="C2")
+    ap.add_argument("--params", choices=("full", "hot"), default="full")
     ap.add_argument("--profile-steps", type=int, default=5, help="steps of the per-kernel event-timed pass")
-    ap.add_argument("--seconds", type=float, default=300.0, help="track length (C2: 300 s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=300.0,
-                    help="CPU baseline sample (default: the whole C2 track)")
+    ap.add_argument("--cpu-chunks", type=int, default=2, help="whole chunks timed on one core (faithful-cost leg)")
+    ap.add_argument("--cpu-procs", type=int, default=0, help="worker processes of the N-core leg (0: the box's "
+                                                              "cores, at most 16)")
+    ap.add_argument("--profile-tag", default=None, help="profiles/<tag>_pmc_summary.json for traffic/limiter")
     return ap.parse_args()
 
 
-def cpu_baseline(pcm, rate, seconds):
-    """The oracle (CPU restatement of the reference chain, 'port'): numpy/scipy
-    stages + the pydub compressor loop in C, one thread, on a prefix of the track."""
-    from oracle import mastering_oracle as mo
-    n = min(int(seconds * rate), pcm.shape[0])
-    sample = np.ascontiguousarray(pcm[:n])
-    mo.master(sample[: rate * 2], rate, P_FULL)  # build / warm caches
-    t0 = time.perf_counter()
-    mo.master(sample, rate, P_FULL)
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "stereo frames/s", "cores": 1, "kind": "port",
-            "sample": f"first {n / rate:.0f} s ({n} frames) of the rank-0 C2 track, full chain (oracle/: "
-                      f"numpy/scipy stages + pydub compressor loop in C + pyloudnorm restatement), 1 thread, "
-                      f"{dt:.2f} s"}
+# ----------------------------------------------------------------- CPU baseline
+def cpu_baseline(args, wl, params):
+    """Faithful-cost CPU path (oracle/faithful_cost.py), 1 core and N cores."""
+    from mastering_amd.synth import pink_noise_pcm16
+    from oracle import faithful_cost
+    rate = wl["rate"]
+    frames = int(wl["seconds"] * rate)
+    pcm = pink_noise_pcm16(frames if wl["seconds"] <= 300 else 300 * rate, rate, 2, track=0)
+    procs = args.cpu_procs or min(16, len(os.sched_getaffinity(0)))
+    r = faithful_cost.time_track(pcm, rate, params, chunks_1core=args.cpu_chunks, procs=procs)
+    scale = frames / pcm.shape[0]  # C4: a 5-min sample track, chunk cost extrapolated to the 2-h track
+    t1 = (r["per_chunk_s_1core"] * r["chunks"] + r["tail_s"]) * scale
+    tn = r.get("track_s_ncore", r["track_s_1core"]) * scale
+    tracks = wl["tracks"]
+    return {"value": tracks * frames / (tn * tracks), "unit": "stereo frames/s", "cores": r.get("procs", 1),
+            "kind": "port",
+            "sample": (f"faithful-cost reference path (numpy/scipy stages + pydub's per-frame Python compressor "
+                       f"loop, pyloudnorm restated): {r['sampled_chunks_1core']} whole 30 s chunks on 1 core "
+                       f"({r['per_chunk_s_1core']:.2f} s each) and {r.get('procs', 1)} chunks on "
+                       f"{r.get('procs', 1)} cores at once ({r.get('wall_s_per_round', 0):.2f} s), the whole-track "
+                       f"tail ({r['tail_s']:.2f} s), extrapolated to the {wl['desc'].split(':')[0]} track "
+                       f"({frames} frames, {r['chunks'] * scale:.0f} chunks)"),
+            "single_core": {"value": frames / t1, "cores": 1, "track_s": t1},
+            "multi_core_track_s": tn, "extrapolated": True}
 
 
-def pmc_traffic(kernel):
+class stdout_to_stderr:
+    """Redirect file descriptor 1 to 2 (native libraries print on it) for a block."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
+# ----------------------------------------------------------------- workloads
+class Runner:
+    """One rank's share of a workload; step() masters it once."""
+
+    def __init__(self, args, wl, params, rank, world, local, dist):
+        import torch
+
+        from mastering_amd import Job, native
+        from mastering_amd.synth import pink_noise_chunks, pink_noise_pcm16
+        self.args, self.wl, self.params, self.rank, self.world = args, wl, params, rank, world
+        self.torch = torch
+        self.dev = f"cuda:{local}"
+        self.ctx = native.context(local)
+        rate = wl["rate"]
+        frames = int(wl["seconds"] * rate)
+        self.kind = args.workload
+        out_kind = native.MM_OUT_F32
+        if self.kind == "C4":
+            from mastering_amd import distributed as D
+            self.D = D
+            self.plan = D.plan_time_shards(frames, rate, 2, world, rank)
+            c0 = self.plan.f0 // (30 * rate)
+            c1 = -(-self.plan.f1 // (30 * rate))
+            pcm = pink_noise_chunks(c0, c1, rate, 2, track=0)
+            self.x = torch.from_numpy(pcm.astype(np.float32) / 32768).to(self.dev)
+            self.out = torch.empty((self.plan.frames, 2), dtype=torch.float32, device=self.dev)
+            uid = D.rccl_unique_id() if rank == 0 else None
+            if world > 1:
+                obj = [uid]
+                dist.broadcast_object_list(obj, src=0)
+                uid = obj[0]
+            with stdout_to_stderr():  # RCCL prints its version banner on stdout: keep stdout the JSON line
+                self.coll = D.LibraryCollectives.create(self.ctx, rank, world, uid)
+            self.backend = D.GpuBackend(self.ctx)
+            self.frames_step = self.plan.frames
+            self.total_frames_step = frames  # the whole track per step (strong scaling)
+            self.jobs = [self.backend.make_job(self.plan, params, out_kind)]
+        else:
+            tracks = wl["tracks"]
+            self.jobs, self.xs, self.outs = [], [], []
+            for t in range(tracks):
+                pcm = pink_noise_pcm16(frames, rate, 2, track=rank * tracks + t)
+                self.xs.append(torch.from_numpy(pcm.astype(np.float32) / 32768).to(self.dev))
+                job = Job(frames, rate, 2, params, out_kind=out_kind)
+                self.jobs.append(job)
+                self.outs.append(torch.empty((job.frames_proc, 2), dtype=torch.float32, device=self.dev))
+            self.frames_step = frames * tracks
+            self.total_frames_step = frames * tracks * world
+        self.results = None
+
+    def step(self, want_results=False):
+        from mastering_amd import engine, native
+        if self.kind == "C4":
+            info = self.D.master_time_sharded(self.backend, self.plan, self.params, self.x.data_ptr(),
+                                              self.out.data_ptr(), self.coll, out_kind=native.MM_OUT_F32)
+            self.ctx.sync()
+            if want_results:
+                self.results = [info]
+        elif len(self.jobs) == 1:
+            res = native.MMResult() if want_results else None
+            engine.master_device(self.ctx, self.jobs[0], self.xs[0].data_ptr(), self.outs[0].data_ptr(), res)
+            if want_results:
+                self.results = [res]
+        else:
+            r = engine.master_batch(self.ctx, self.jobs, [x.data_ptr() for x in self.xs],
+                                    [o.data_ptr() for o in self.outs], with_results=want_results)
+            if want_results:
+                self.results = r
+
+
+def profile_summary(tag):
+    path = os.path.join(ROOT, "profiles", f"{tag}_pmc_summary.json")
     try:
-        with open(PMC_SUMMARY) as f:
-            k = json.load(f)["kernels"].get(kernel)
-    except (OSError, ValueError, KeyError):
-        return None
-    return None if k is None else k.get("bytes_per_launch")
+        with open(path) as f:
+            return json.load(f), path
+    except (OSError, ValueError):
+        return None, path
 
 
 def main():
@@ -115,30 +250,24 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    wl = WORKLOADS[args.workload]
+    params = P_HOT if args.params == "hot" else P_FULL
+
+    # the CPU baseline first: its worker processes fork before anything initialises the GPU
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, wl, params)
+
     import torch
     import torch.distributed as dist
-
     if world > 1:
-        dist.init_process_group("gloo")  # control plane only (barrier, max of timings)
+        dist.init_process_group("gloo")  # control plane only (barrier, max of timings, RCCL id broadcast)
     torch.cuda.set_device(local)
-
-    from mastering_amd import Job, engine, native
-    from mastering_amd.synth import pink_noise_pcm16
-
-    rate = 44100
-    frames = int(args.seconds * rate)
-    pcm = pink_noise_pcm16(frames, rate, 2, track=rank)
-    x = torch.from_numpy(np.ascontiguousarray(pcm.astype(np.float32) / 32768)).to(f"cuda:{local}")
-    job = Job(frames, rate, 2, P_FULL, out_kind=native.MM_OUT_F32)
-    out = torch.empty((job.frames_proc, 2), dtype=torch.float32, device=f"cuda:{local}")
-    ctx = native.context(local)
-
-    def step(res=None):
-        return engine.master_device(ctx, job, x.data_ptr(), out.data_ptr(), res)
+    run = Runner(args, wl, params, rank, world, local, dist if world > 1 else None)
 
     for _ in range(args.warmup):
-        step()
-    ctx.sync()
+        run.step()
+    run.ctx.sync()
     torch.cuda.synchronize()
 
     # ---- timed region: no instrumentation
@@ -147,8 +276,8 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
-    ctx.sync()
+        run.step()
+    run.ctx.sync()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
@@ -160,48 +289,81 @@ def main():
         dt = float(t.item())
 
     # ---- profiling pass: HIP events around every launch
-    res = native.MMResult()
-    ctx.timing(True)
-    for i in range(args.profile_steps):
-        step(res if i == args.profile_steps - 1 else None)
-    stats = ctx.kernel_stats()
-    ctx.timing(False)
+    run.ctx.timing(True)
+    P = max(1, args.profile_steps)
+    for i in range(P):
+        run.step(want_results=(i == P - 1))
+    stats = run.ctx.kernel_stats()
+    run.ctx.timing(False)
 
     if rank == 0:
-        P = args.profile_steps
-        total_frames = frames * world * args.steps
-        value = total_frames / dt
+        from mastering_amd import native
+        ms_step = dt / args.steps * 1e3
+        value = run.total_frames_step * args.steps / dt
         per = {k: (ms / P, n / P) for k, (ms, n) in stats.items()}  # per step: ms, launches
         dom = max(per, key=lambda k: per[k][0])
-        ms_step, launches = per[dom]
-        avg_s = ms_step / 1e3 / max(launches, 1)
-        walked_per_launch = res.comp_walked / max(launches, 1) if dom == "comp_fix" else 0
-        bpl = algorithmic_bytes(dom, job.frames_proc, job.G, res.comp_active, walked_per_launch)
-        achieved = bpl / avg_s / 1e9 if bpl is not None else None
-        traffic = pmc_traffic(dom)
-        dev_ms = sum(v[0] for v in per.values())
+        dom_ms, launches = per[dom]
+        avg_s = dom_ms / 1e3 / max(launches, 1)
+        res = run.results
+        active = sum(int(getattr(r, "comp_active", 0) or 0) for r in res) if res and not isinstance(res[0], dict) \
+            else 0
+        walked = sum(int(getattr(r, "comp_walked", 0) or 0) for r in res) if res and not isinstance(res[0], dict) \
+            else 0
+        iters = [int(r.comp_iters) for r in res] if res and not isinstance(res[0], dict) else None
+        job0 = run.jobs[0]
+        n_frames = run.frames_step
+        g_tiles = sum(j.G for j in run.jobs)
+        walked_per_launch = walked / max(launches, 1) if dom == "comp_fix" else 0
+        bpl = algorithmic_bytes(dom, n_frames, g_tiles, active, walked_per_launch)
+        k_achieved = bpl / avg_s / 1e9 if bpl is not None else None
+        chain_gbs = CHAIN_BYTES_PER_FRAME * n_frames / (ms_step / 1e3) / 1e9
+        # PMC traffic and SQ shares, only from a profile of these exact sources
+        sha = source_sha()
+        tag = args.profile_tag or f"r02_{args.workload}" + ("hot" if args.params == "hot" else "")
+        prof, prof_path = profile_summary(tag)
+        traffic = limiter = dom_traffic = None
+        prof_note = f"no profile at {os.path.relpath(prof_path, ROOT)}"
+        if prof is not None:
+            if prof.get("source_sha") != sha:
+                prof_note = (f"{os.path.relpath(prof_path, ROOT)} was measured on sources {prof.get('source_sha')}, "
+                             f"these are {sha}: traffic not reported")
+            else:
+                prof_note = os.path.relpath(prof_path, ROOT)
+                traffic = prof.get("chain", {}).get("bytes_per_step")
+                limiter = prof.get("chain", {}).get("limiter")
+                k = prof.get("kernels", {}).get(dom, {})
+                dom_traffic = k.get("bytes_per_launch")
         line = {
             "metric": METRIC, "value": value, "unit": "stereo frames/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": "C2: 5-min 44.1 kHz stereo f32 pink-noise track per GPU, full chain "
-                                   "(sat 30, techno EQ, width 1.3, multiband defaults, LUFS -14)",
-                       "frames_per_track": frames, "tracks_per_gpu": 1, "rate": rate,
-                       "parallelism": f"file-sharded x{world}", "out": "f32 interleaved (decoded PCM16)"},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS if achieved is not None else None,
-                         "traffic": traffic, "algorithmic_bytes_per_launch": bpl,
-                         "avg_launch_ms": avg_s * 1e3, "launches_per_step": launches,
-                         "note": ENVELOPE_NOTE if dom in ("comp_pass0", "comp_fix", "comp_record") else None},
-            "chain": {"algorithmic_bytes_per_frame": 16, "device_ms_per_step": dev_ms,
-                      "achieved_GBps": 16 * job.frames_proc / (dt / args.steps) / 1e9,
-                      "frac_of_peak": 16 * job.frames_proc / (dt / args.steps) / 1e9 / HBM_PEAK_GBS,
-                      "comp_iters": res.comp_iters, "comp_active_frames": res.comp_active,
-                      "comp_rewalked_frames": res.comp_walked,
+            "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
+            "scaling": "strong" if args.workload == "C4" else "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": wl["desc"] + (", full chain P_HOT thresholds" if args.params == "hot" else
+                                                 ", full chain (sat 30, techno EQ, width 1.3, multiband defaults, "
+                                                 "LUFS -14)"),
+                       "frames_per_track": int(wl["seconds"] * wl["rate"]), "tracks_per_gpu": wl["tracks"],
+                       "rate": wl["rate"], "frames_per_rank_step": n_frames,
+                       "parallelism": (f"time-sharded x{world} (library RCCL)" if args.workload == "C4"
+                                       else f"file-sharded x{world}"),
+                       "in": "f32 interleaved (decoded PCM16)", "out": "f32 interleaved"},
+            "roofline": {"bound": "hbm", "limiter": limiter, "achieved": chain_gbs, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": chain_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                         "algorithmic_bytes_per_step": CHAIN_BYTES_PER_FRAME * n_frames,
+                         "scope": "whole chain: 16 B per stereo frame over ms_per_step",
+                         "profile": prof_note, "source_sha": sha,
+                         "dominant_kernel": {"name": dom, "achieved": k_achieved,
+                                             "frac": k_achieved / HBM_PEAK_GBS if k_achieved else None,
+                                             "algorithmic_bytes_per_launch": bpl, "avg_launch_ms": avg_s * 1e3,
+                                             "launches_per_step": launches, "traffic": dom_traffic}},
+            "chain": {"device_ms_per_step": sum(v[0] for v in per.values()),
+                      "comp_iters": iters, "comp_active_frames": active, "comp_rewalked_frames": walked,
                       "kernels_ms_per_step": {k: round(v[0], 4) for k, v in per.items()}},
         }
-        if not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(pcm, rate, args.cpu_seconds)
+        if args.workload == "C4":
+            line["chain"]["loudness"] = res[0]["loudness"] if res else None
+        if cpu is not None:
+            line["cpu_baseline"] = cpu
+        del native
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -139,6 +139,13 @@ int mm_master(mm_ctx *ctx, const mm_job *job, const void *in, void *out, mm_resu
 /* Same, with device-resident input/output (zero-copy; e.g. torch tensors). */
 int mm_master_device(mm_ctx *ctx, const mm_job *job, const void *d_in, void *d_out, mm_result *res);
 
+/* A batch of independent tracks (file sharding, BASELINE C3/C5): jobs[i] with
+ * device input d_in[i] and output d_out[i]; up to MM_BATCH_STREAMS tracks run at
+ * once on streams of their own (child contexts), res[i] (optional) as above. */
+#define MM_BATCH_STREAMS 8
+int mm_master_batch(mm_ctx *ctx, int n, const mm_job *jobs, const void *const *d_in, void *const *d_out,
+                    mm_result *res);
+
 /* ---- WAV files (AME:43 decode, AME:98 export) ------------------------------ */
 typedef struct mm_wav_info {
     int64_t frames;          /* whole frames in the data chunk                   */

@@ -135,12 +135,17 @@ struct CompArgs {
     double attack_frames[3], release_frames[3];
     double rcp_attack[3], rcp_release[3];
     uint16_t *r16[3];          // tile-major audioop.rms per frame
+    const double *E[3], *tail[3];  // per tile: sum of L^2+R^2, and over its last look % T frames
     int32_t *cnt[3];           // per tile: active frames
     int32_t *off[3];           // per tile: compacted index of its first active frame (in chunk)
     int32_t *total[3];         // per chunk: active frames
     double *Mc[3];             // compacted M of active frames, super-tile-major [U + 1][GS]
+    double *ck[3];             // envelope checkpoints: state on entry to compacted rows o = 0, Q, 2Q, ...
+                               // of every super-tile, [U / Q][GS] (written by the owning walks)
+    int own;                   // super-tiles walked per pass-0 lane (after one warm-up)
+    int64_t ocols;             // ceil(GS / own): pass-0 lanes per band
+    int64_t RS;                // row stride of Mc / ck (own * ocols >= GS columns)
     double *start[3];          // per-super-tile start state
-    double *tstart[3];         // per-tile start state (comp_record)
     const double *end_in[3];
     double *end_out[3];
     unsigned int *changed;

@@ -26,11 +26,14 @@
 //  5. comp_fix     Jacobi sweeps: a super-tile whose start differs from its
 //                  predecessor's end re-walks from it; at the fixed point every
 //                  start is the true state (induction from the chunk start);
-//  6. comp_record  one walk from the converged starts overwrites Mc with the
-//                  att after every active frame; comp_tstart gathers each
-//                  tile's starting att from it;
-//  7. comp_apply   per (tile, band): exact trajectory, gains, audioop.mul,
-//                  overlay through LDS.
+//     Every walk that OWNS a super-tile (pass 0's own walks, the sweeps'
+//     re-walks) stores a checkpoint: the state on entry to every Q-th compacted
+//     frame.  The last walk of a super-tile starts from its converged start, so
+//     at the fixed point every checkpoint is exact;
+//  6. comp_apply   per (tile, band): the tile's starting state from the
+//                  checkpoint at or before its first compacted frame plus < Q
+//                  steps, then the exact trajectory, gains, audioop.mul, overlay
+//                  through LDS.
 // Sparse bands (the high band is active on ~0.1 % of pink-noise frames) thus
 // cost a few super-tiles per chunk, and dense ones ~frames/U.
 #include "common.h"
@@ -70,16 +73,16 @@ __global__ void __launch_bounds__(256) comp_rms_kernel(CompArgs a) {
     const int64_t f0 = g * T;
     const int64_t chunk0 = (g / a.K) * a.K * T;
     const int len = (int)min((int64_t)T, a.N_proc - f0);
-    // warm-up: S over [lo0, f0)
+    // S over [lo0, f0): the look / T whole tiles before this one plus the last
+    // look % T frames of the one before them, from the crossover's per-tile sums
+    // (tiles never straddle a chunk start, so the chunk clamp is per tile)
     const int64_t lo0 = max(chunk0, f0 - look);
-    const uint32_t gw = (uint32_t)(lo0 / T);
     double S = 0.0;
     {
-        uint32_t gt = gw, n = (uint32_t)(lo0 - (int64_t)gw * T);
-        for (; gt < g32; ++gt, n = 0) {  // <= look/T + 1 tiles
-#pragma unroll 5
-            for (; n < (uint32_t)T; ++n) S += (double)frame_energy(x[n * G + gt]);
-        }
+        const int kf = look / T;
+        for (int t = 1; t <= kf; ++t)
+            if ((g - t) * T >= chunk0) S += a.E[b][g - t];
+        if (look % T != 0 && (g - kf - 1) * T >= chunk0) S += a.tail[b][g - kf - 1];
     }
     // drop frames: d = f - look for f >= chunk0 + look; the first `skip` frames drop nothing
     const int64_t d_first = max(f0 - look, chunk0);
@@ -151,6 +154,14 @@ __global__ void __launch_bounds__(1024) comp_offsets_kernel(CompArgs a) {
     if (tid == 1023) a.total[b][blockIdx.x] = buf[1023];
 }
 
+// Column of super-tile s in Mc / ck: pass-0 lane j owns super-tiles j*own ..
+// j*own + own-1, so super-tile j*own + t lives in column t*ocols + j and the 64
+// lanes of a wave touch 64 consecutive columns (512 contiguous bytes) at every
+// step of every walk, whatever `own` is.
+__device__ __forceinline__ int64_t cm_col(const CompArgs &a, int64_t s) {
+    return (s % a.own) * a.ocols + s / a.own;
+}
+
 // 3. scatter M of active frames into the compacted array.  grid (ceil(G/256), 3)
 // Inactive frames store into this lane's own padding slot (row U of the array),
 // so every store is unconditional; the element index is 32-bit and advanced
@@ -160,7 +171,8 @@ __global__ void __launch_bounds__(256) comp_compact_kernel(CompArgs a) {
     const int b = blockIdx.y;
     if (g >= a.G) return;
     if (a.cnt[b][g] == 0) return;
-    const uint32_t G32 = (uint32_t)a.G, g32 = (uint32_t)g, GS = (uint32_t)a.GS, U = (uint32_t)a.U;
+    const uint32_t G32 = (uint32_t)a.G, g32 = (uint32_t)g, RS = (uint32_t)a.RS, U = (uint32_t)a.U;
+    const uint32_t own = (uint32_t)a.own, ocols = (uint32_t)a.ocols;
     const uint16_t *R = a.r16[b] + g32;
     const double *lut = a.lut[b];
     const uint32_t r0 = a.r0[b];
@@ -168,8 +180,9 @@ __global__ void __launch_bounds__(256) comp_compact_kernel(CompArgs a) {
     const uint32_t p = (uint32_t)a.off[b][g];
     uint32_t k = p / U, o = p - k * U;  // super-tile and row of the next active frame
     const uint32_t base = (uint32_t)(g / a.K) * (uint32_t)a.SPC;
-    uint32_t idx = o * GS + base + k;  // its element
-    const uint32_t dummy = U * GS + g32 % GS;
+    uint32_t sg = base + k, t = sg % own, col = t * ocols + sg / own;  // its super-tile, column
+    uint32_t idx = o * RS + col;  // its element
+    const uint32_t dummy = U * RS + g32 % RS;
     double *Mc = a.Mc[b];
     stream2<8, 2, uint16_t, double>(
         len, [&](int i) { return R[(uint32_t)min(i, len - 1) * G32]; },
@@ -180,8 +193,12 @@ __global__ void __launch_bounds__(256) comp_compact_kernel(CompArgs a) {
             Mc[(idx & amask) | (dummy & ~amask)] = m;
             const uint32_t o1 = o + act;
             const uint32_t wmask = 0u - (o1 == U ? 1u : 0u);  // the super-tile is full
-            idx = ((idx + (GS & amask)) & ~wmask) | ((base + k + 1u) & wmask);
-            k -= wmask;  // + 1 on a wrap
+            // next super-tile's column: +ocols within a lane's group, else the next lane's first
+            const uint32_t tw = 0u - (t + 1u == own ? 1u : 0u);
+            const uint32_t ncol = ((col + ocols) & ~tw) | ((col - t * ocols + 1u) & tw);
+            idx = ((idx + (RS & amask)) & ~wmask) | (ncol & wmask);
+            col = (col & ~wmask) | (ncol & wmask);
+            t = (t & ~wmask) | (((t + 1u) & ~tw) & wmask);
             o = o1 & ~wmask;
         });
 }
@@ -263,19 +280,21 @@ __device__ __forceinline__ double lean_step(double att, double m, double inc, do
 // ahead in registers; the two divisions run WP frames ahead of the step that
 // uses them, so they issue while the att chain of earlier frames is in flight
 // (in-order issue: tools/micro/walk2_bench.hip, 136 -> 98 cycles per step).
-// With STORE, overwrite each compacted M with the att after that frame.
+// With CK (an owning walk), store the state on entry to every CK_Q-th frame.
 constexpr int WALK_WB = 32;  // M values in flight per walker
 constexpr int WALK_PAD = WALK_WB;  // padding rows after the compacted array (prefetch past a super-tile's end)
+constexpr int CK_Q = 8;      // checkpoint stride (compacted frames); divides WALK_WB, FIX_CHUNK and U
 
-template <bool STORE>
+template <bool CK>
 __device__ __forceinline__ double comp_walk(double att, const CompArgs &a, int b, int64_t s, int len,
                                             const BandStep &bs) {
     constexpr int WB = WALK_WB, WP = 4;
     if (len <= 0) return att;
     // column s, rows GS apart; loads run up to WB rows past the end (padding rows)
-    const size_t GS = (size_t)a.GS;
-    const double *pl = a.Mc[b] + s;
-    double *ps = a.Mc[b] + s;
+    const size_t GS = (size_t)a.RS;  // row stride
+    const int64_t cs = cm_col(a, s);
+    const double *pl = a.Mc[b] + cs;
+    double *pc = CK ? a.ck[b] + cs : nullptr;  // checkpoint rows, one row stride apart
     double buf[WB], inc[WP], dec[WP];
 #pragma unroll
     for (int k = 0; k < WB; ++k) {
@@ -295,11 +314,11 @@ __device__ __forceinline__ double comp_walk(double att, const CompArgs &a, int b
             const double mn = buf[(k + WP) % WB];  // frame i+k+WP (already reloaded when k+WP >= WB)
             inc[k % WP] = div_cr(mn, bs.A, bs.rA);
             dec[k % WP] = div_cr(mn, bs.R, bs.rR);
-            att = lean_step(att, m, ik, dk);
-            if (STORE) {
-                *ps = att;
-                ps += GS;
+            if (CK && k % CK_Q == 0) {
+                *pc = att;
+                pc += GS;
             }
+            att = lean_step(att, m, ik, dk);
             buf[k] = *pl;
             pl += GS;
         }
@@ -312,52 +331,56 @@ __device__ __forceinline__ double comp_walk(double att, const CompArgs &a, int b
             const double mn = buf[(k + WP) % WB];
             inc[k % WP] = div_cr(mn, bs.A, bs.rA);
             dec[k % WP] = div_cr(mn, bs.R, bs.rR);
-            att = lean_step(att, m, ik, dk);
-            if (STORE) {
-                *ps = att;
-                ps += GS;
+            if (CK && k % CK_Q == 0) {
+                *pc = att;
+                pc += GS;
             }
+            att = lean_step(att, m, ik, dk);
         }
     }
     return att;
 }
 
-// Compact streamed walk (no STORE) for the fix kernel's lane path, where the
-// register budget is shared with the LDS-staged path.
+// Compact streamed owning walk (checkpoints) for the fix kernel's lane path,
+// where the register budget is shared with the LDS-staged path.
 __device__ __forceinline__ double comp_walk_lean(double att, const CompArgs &a, int b, int64_t s, int len,
                                                  const BandStep &bs) {
-    const double *col = a.Mc[b] + s;
-    const uint32_t GS = (uint32_t)a.GS;
+    const int64_t cs = cm_col(a, s);
+    const double *col = a.Mc[b] + cs;
+    double *ck = a.ck[b] + cs;
+    const uint32_t GS = (uint32_t)a.RS;
+    int i = 0;
     stream<8, 4, double>(
-        len, [&](int i) { return col[(uint32_t)min(i, len - 1) * GS]; },
-        [&](double m) { att = comp_step(att, m, bs); });
+        len, [&](int k) { return col[(uint32_t)min(k, len - 1) * GS]; },
+        [&](double m) {
+            if (i % CK_Q == 0) ck[(uint32_t)(i / CK_Q) * GS] = att;
+            att = comp_step(att, m, bs);
+            ++i;
+        });
     return att;
 }
 
-// 4. speculative pass.  grid: (ceil(GS/(OWN*BLOCK)), 3).  Each lane walks OWN
+// 4. speculative pass.  grid: (ceil(GS/(own*BLOCK)), 3).  Each lane walks `own`
 // consecutive super-tiles.  The start of the first is guessed by walking the
 // `warmup` previous super-tiles of its chunk, from the M of the first warm-up
 // frame (the state tracks M closely: this coalesces with the true trajectory far
 // more often than a start at 0; tools/ studies); the later ones start from the
-// end of the one before (a longer warm-up for free).  OWN > 1 divides the
-// warm-up walks (and their M re-reads) by OWN.
-#ifndef MM_PASS0_OWN
-#define MM_PASS0_OWN 2
-#endif
+// end of the one before (a longer warm-up for free).  own > 1 divides the
+// warm-up walks (and their M re-reads) by own; the host raises it with the
+// problem size (more super-tiles than the chip needs lanes).
 #ifndef MM_PASS0_BLOCK
 #define MM_PASS0_BLOCK 64
 #endif
-constexpr int PASS0_OWN = MM_PASS0_OWN;
 constexpr int PASS0_BLOCK = MM_PASS0_BLOCK;
 
 __global__ void __launch_bounds__(PASS0_BLOCK) comp_pass0_kernel(CompArgs a) {
-    const int64_t s0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * PASS0_OWN;
+    const int64_t s0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * a.own;
     const int b = blockIdx.y;
     if (s0 >= a.GS) return;
     const BandStep bs = band_step(a, b);
     double att = 0.0;
     bool warm = false;
-    for (int64_t s = s0; s < min(s0 + PASS0_OWN, a.GS); ++s) {
+    for (int64_t s = s0; s < min(s0 + a.own, a.GS); ++s) {
         const Super st = super_of(a, b, s);
         if (st.len == 0) {
             warm = false;
@@ -368,13 +391,13 @@ __global__ void __launch_bounds__(PASS0_BLOCK) comp_pass0_kernel(CompArgs a) {
         } else if (!warm && a.warmup > 0) {
             const int64_t k = st.p0 / a.U;  // index of s within its chunk
             const int64_t w0 = s - min((int64_t)a.warmup, k);
-            att = a.Mc[b][w0];  // row 0 of super-tile w0
+            att = a.Mc[b][cm_col(a, w0)];  // row 0 of super-tile w0
             for (int64_t w = w0; w < s; ++w) att = comp_walk<false>(att, a, b, w, a.U, bs);
         } else if (!warm) {
             att = 0.0;
         }
         a.start[b][s] = att;
-        att = comp_walk<false>(att, a, b, s, st.len, bs);
+        att = comp_walk<true>(att, a, b, s, st.len, bs);
         a.end_out[b][s] = att;
         warm = true;
     }
@@ -395,6 +418,7 @@ constexpr int FIX_MAX_U = 8192; // cap on frames per super-tile (slot lengths ar
 __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned int *prev_changed) {
     __shared__ double sm[FIX_SLOTS][FIX_CHUNK + 1], si[FIX_SLOTS][FIX_CHUNK + 1], sd[FIX_SLOTS][FIX_CHUNK + 1];
     __shared__ int slot_lane[FIX_SLOTS], slot_len[FIX_SLOTS];
+    __shared__ int64_t slot_col[FIX_SLOTS];
     if (prev_changed && *prev_changed == 0u) return;
     const int lane = threadIdx.x;
     const int64_t s = (int64_t)blockIdx.x * 64 + lane;
@@ -420,6 +444,7 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
         if (need) {
             slot_lane[slot] = lane;
             slot_len[slot] = st.len;
+            slot_col[slot] = cm_col(a, s);
         }
         __syncthreads();
         int maxlen = 0;
@@ -432,7 +457,7 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
             for (int r = 0; r < FIX_SLOTS; ++r) {
                 if (r < k) {
                     const int i = base + lane;
-                    pre[r] = i < slot_len[r] ? Mc[(int64_t)i * a.GS + col0 + slot_lane[r]] : 0.0;
+                    pre[r] = i < slot_len[r] ? Mc[(int64_t)i * a.RS + slot_col[r]] : 0.0;
                 }
             }
         };
@@ -453,8 +478,10 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
             if (need) {
                 const int lim = min(FIX_CHUNK, st.len - base);
                 const double *pm = sm[slot], *pi = si[slot], *pd = sd[slot];
+                double *ck = a.ck[b] + slot_col[slot] + (int64_t)(base / CK_Q) * a.RS;
 #pragma unroll 8
                 for (int f = 0; f < lim; ++f) {
+                    if (f % CK_Q == 0) ck[(int64_t)(f / CK_Q) * a.RS] = att;  // base is a multiple of CK_Q
                     const double up = fmin(att + pi[f], pm[f]);
                     const double dn = fmax(att - pd[f], 0.0);
                     att = att <= pm[f] ? up : dn;
@@ -472,35 +499,25 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
     if (live) a.end_out[b][s] = e;
 }
 
-// 6. exact att after every active frame (Mc is overwritten in place).
-#ifndef MM_RECORD_BLOCK
-#define MM_RECORD_BLOCK 256
-#endif
-constexpr int RECORD_BLOCK = MM_RECORD_BLOCK;  // lanes (super-tiles) per block: few blocks spread over more CUs
-
-__global__ void __launch_bounds__(RECORD_BLOCK) comp_record_kernel(CompArgs a) {
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int b = blockIdx.y;
-    if (s >= a.GS) return;
-    const Super st = super_of(a, b, s);
-    if (st.len == 0) return;
-    comp_walk<true>(st.p0 > 0 ? a.start[b][s] : 0.0, a, b, s, st.len, band_step(a, b));
-}
-
 // compacted index p of chunk c -> element address in the super-tile-major array
 __device__ __forceinline__ int64_t cm_index(const CompArgs &a, int64_t c, int32_t p) {
     const int32_t k = p / a.U, o = p - k * a.U;
-    return (int64_t)o * a.GS + c * a.SPC + k;
+    return (int64_t)o * a.RS + cm_col(a, c * a.SPC + k);
 }
 
-// 6b. per tile: att at its first frame = att after compacted frame off-1 (0 if
-// the chunk had no active frame before it).  grid (ceil(G/256), 3)
-__global__ void __launch_bounds__(256) comp_tstart_kernel(CompArgs a) {
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int b = blockIdx.y;
-    if (g >= a.G) return;
-    const int32_t p = a.off[b][g];
-    a.tstart[b][g] = p > 0 ? a.Mc[b][cm_index(a, g / a.K, p - 1)] : 0.0;
+// State on entry to compacted frame p of chunk c (the start of the tile whose
+// first active frame is p): the checkpoint at or before p, then < CK_Q steps.
+// p == total active frames of the chunk (a tile after its last active frame)
+// uses the checkpoint before it (the one at p itself belongs to no walk).
+__device__ __forceinline__ double comp_state_at(const CompArgs &a, int b, int64_t c, int32_t p, const BandStep &bs) {
+    if (p <= 0) return 0.0;
+    const int32_t L = a.total[b][c];
+    int32_t q = p - p % CK_Q;
+    if (q >= L) q -= CK_Q;
+    const int32_t k = q / a.U, o = q - k * a.U;
+    double att = a.ck[b][(int64_t)(o / CK_Q) * a.RS + cm_col(a, c * a.SPC + k)];
+    for (int32_t i = q; i < p; ++i) att = comp_step(att, a.Mc[b][cm_index(a, c, i)], bs);
+    return att;
 }
 
 // 7. gains + overlay.  A block = 64 tiles x 3 bands: wave w runs band w's exact
@@ -534,7 +551,8 @@ __global__ void __launch_bounds__(192) comp_apply_kernel(CompArgs a) {
     const BandStep bs = band_step(a, b);
     const uint16_t *R = a.r16[b];
     const short2 *X = a.band[b];
-    double att = valid ? a.tstart[b][g] : 0.0;
+    double att = valid ? comp_state_at(a, b, g / a.K, a.off[b][g], bs) : 0.0;
+    double gain = 1.0, gain_att = -1.0;  // gain = db_to_float(-gain_att); att >= 0 never equals -1
     uint16_t rn[APPLY_STEP];
     short2 vn[APPLY_STEP];
     auto prefetch = [&](int n0) {
@@ -559,10 +577,15 @@ __global__ void __launch_bounds__(192) comp_apply_kernel(CompArgs a) {
 #pragma unroll
         for (int j = 0; j < APPLY_STEP; ++j) {
             if (n0 + j < len) {
-                att = comp_step(att, m[j], bs);
+                // M == 0 (rms <= threshold) is the identity step, and the gain only
+                // changes with att: the sparse band's wave skips both almost always
+                if (m[j] != 0.0) att = comp_step(att, m[j], bs);
                 short2 s = v[j];
                 if (att != 0.0) {
-                    const double gain = exp10(neg_div20(att));  // db_to_float(-att)
+                    if (att != gain_att) {
+                        gain = exp10(neg_div20(att));  // db_to_float(-att)
+                        gain_att = att;
+                    }
                     s.x = audioop_mul(s.x, gain);
                     s.y = audioop_mul(s.y, gain);
                 }

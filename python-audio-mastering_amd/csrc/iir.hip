@@ -69,6 +69,7 @@ struct EqArgs {
     int width_on;
     double sos[4][5];  // {b0,b1,b2,a1,a2}
     int16_t *q_out;    // tile-major int16 pairs
+    float *xs;         // tile-major f32 scratch: pass 1 leaves the exciter's output here for pass 2
 };
 
 template <int CH>
@@ -145,6 +146,7 @@ __device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, doub
             if (n >= len) break;
             float x = row[j * CH + c];
             if (a.sat.on) x = saturate(x, a.sat);
+            if (!P2) a.xs[((int64_t)n * a.G + g0 + t) * CH + c] = x;  // pass 2 reads it back coalesced
             double y = (double)x;
 #pragma unroll
             for (int s = 0; s < NS; ++s) y = df2t(y, z[s][0], z[s][1], sos[s]);
@@ -164,6 +166,35 @@ __device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, doub
         if (step + 1 < nsteps) store(cur ^ 1);
         lds_barrier();
     }
+}
+
+// Pass 2 from the tile-major exciter output pass 1 left in a.xs: the lane's own
+// frames, 64 lanes reading 256 contiguous bytes per step, no LDS staging, barrier
+// or second tanh.  EQ -> width (lane-pair exchange) -> int16.
+template <int NS, int CH>
+__device__ void eq_pass2(const EqArgs &a, int64_t g, int c, int len, double (&z)[NS][2]) {
+    const double(*sos)[5] = a.sos;
+    const int64_t G = a.G;
+    const float *xs = a.xs;
+    int n = 0;
+    stream<8, 3, float>(
+        len, [&](int i) { return xs[((int64_t)min(i, len - 1) * G + g) * CH + c]; },
+        [&](float x) {
+            double y = (double)x;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) y = df2t(y, z[s][0], z[s][1], sos[s]);
+            if (CH == 2 && a.width_on) {  // apply_stereo_width (AME:136-144), f64
+                const double o = __shfl_xor(y, 1);
+                const double yl = c == 0 ? y : o, yr = c == 0 ? o : y;
+                const double mid = (yl + yr) / 2;
+                const double side = (yl - yr) / 2 * a.width;
+                y = c == 0 ? mid + side : mid - side;
+            }
+            const int64_t o = ((int64_t)n * G + g) * 2;
+            if (CH == 2) a.q_out[o + c] = quantize(y);
+            else *reinterpret_cast<short2 *>(a.q_out + o) = make_short2(quantize(y), 0);  // mono: R = 0
+            ++n;
+        });
 }
 
 // I16: the input is int16 PCM (a.in16), else f32 (a.in); a template parameter so
@@ -205,7 +236,7 @@ __global__ void __launch_bounds__(LB_THREADS, 4) eq_kernel(EqArgs a, LbArgs lb, 
         zs[s_][0] = s[2 * s_];
         zs[s_][1] = s[2 * s_ + 1];
     }
-    eq_pass<NS, CH, true, I16>(a, g0, t, c, len, zs, stage);
+    if (valid) eq_pass2<NS, CH>(a, g, c, len, zs);
 }
 
 // No active EQ stage: the chain stays f32 (AME:152-162 returns the f32 input;
@@ -251,13 +282,26 @@ struct XoArgs {
     double sos[4][5];     // LP s0, LP s1, HP s0, HP s1
     const int16_t *q_in;  // tile-major int16 pairs
     int16_t *band[3];     // low / mid / high planes, same layout
+    // per tile and band, for the compressor's RMS windows (exact integer sums in
+    // f64): E = sum of L^2 + R^2 over the tile, tail = the same over its last
+    // frames n >= tail_from (the window's partial tile, look % T frames)
+    double *E[3], *tail[3];
+    int tail_from[3];
 };
+
+template <int CH>
+__device__ __forceinline__ double frame_energy2(int16_t q) {  // L^2 + R^2 of the lane pair (mono: q^2)
+    const int32_t v = q;
+    const int32_t w = CH == 2 ? __shfl_xor(v, 1) : 0;
+    return (double)((uint32_t)(v * v) + (uint32_t)(w * w));
+}
 
 template <int CH, bool P2>
 __device__ __forceinline__ void xo_pass(const XoArgs &a, int64_t g, int c, int len, double (&z)[4][2]) {
     const double(*sos)[5] = a.sos;
     const int64_t G = a.G;
     int pn = 0;
+    double E[3] = {0.0, 0.0, 0.0}, tl[3] = {0.0, 0.0, 0.0};
     stream<8, MM_XO_NB, int16_t>(
         len, [&](int i) { return a.q_in[((int64_t)min(i, len - 1) * G + g) * 2 + c]; },
         [&](int16_t q) {
@@ -269,18 +313,30 @@ __device__ __forceinline__ void xo_pass(const XoArgs &a, int64_t g, int c, int l
             if (P2) {
                 const double ym = (x - yl) - yh;  // AME:202
                 const int64_t o = ((int64_t)pn * G + g) * 2;
+                const int16_t q[3] = {quantize(yl), quantize(ym), quantize(yh)};
                 if (CH == 2) {
-                    a.band[0][o + c] = quantize(yl);
-                    a.band[1][o + c] = quantize(ym);
-                    a.band[2][o + c] = quantize(yh);
+#pragma unroll
+                    for (int b = 0; b < 3; ++b) a.band[b][o + c] = q[b];
                 } else {  // mono: the second half of every pair stays 0
-                    *reinterpret_cast<short2 *>(a.band[0] + o) = make_short2(quantize(yl), 0);
-                    *reinterpret_cast<short2 *>(a.band[1] + o) = make_short2(quantize(ym), 0);
-                    *reinterpret_cast<short2 *>(a.band[2] + o) = make_short2(quantize(yh), 0);
+#pragma unroll
+                    for (int b = 0; b < 3; ++b) *reinterpret_cast<short2 *>(a.band[b] + o) = make_short2(q[b], 0);
+                }
+#pragma unroll
+                for (int b = 0; b < 3; ++b) {
+                    const double e = frame_energy2<CH>(q[b]);
+                    E[b] += e;
+                    tl[b] += pn >= a.tail_from[b] ? e : 0.0;
                 }
             }
             ++pn;
         });
+    if (P2 && c == 0) {
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            a.E[b][g] = E[b];
+            a.tail[b][g] = tl[b];
+        }
+    }
 }
 
 template <int CH>

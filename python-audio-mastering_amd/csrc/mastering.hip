@@ -79,6 +79,13 @@ struct mm_ctx {
     // host tables already resident on the device
     const double *lut_src[3] = {nullptr, nullptr, nullptr};  // host tables already on the device
     std::map<std::string, std::vector<double>> mats_cache;
+    // pinned block the chain's results are copied into (one sync per chain)
+    char *rb = nullptr;
+    size_t rb_cap = 0;
+    // batch execution (mm_master_batch): child contexts, one stream each
+    std::vector<mm_ctx *> children;
+    int concurrency = 1;  // chains running beside this one (batch streams): sizes pass-0 ownership
+    int own_override = 0;  // MM_PASS0_OWN (tuning): fixed pass-0 ownership
     // rccl
     ncclComm_t comm = nullptr;
     int rank = 0, nranks = 1;
@@ -288,12 +295,10 @@ static int launch_eq(mm_ctx *c, int nsec, int ch, unsigned nblk, const EqArgs &e
 // at once if sweep k-1 changed nothing (so after the first quiet sweep both end
 // buffers hold the converged ends).  Convergence is checked at the chain's
 // single sync (comp_check); a rare unconverged batch is extended there.
-constexpr int COMP_SWEEPS = 6;  // queued per chain; more resume from the host (re-compact + sweeps)
+constexpr int COMP_SWEEPS = 6;  // queued per chain; more resume from the host (more sweeps, then apply again)
 
-static int comp_sweeps(mm_ctx *c, int n, bool resume = false) {
+static int comp_sweeps(mm_ctx *c, int n) {
     CompArgs &ca = c->ca;
-    // comp_record overwrote Mc with attenuations: restore M before resuming
-    if (resume) RET(launch(c, "comp_compact", comp_compact_kernel, dim3(c->comp_nb, 3), dim3(256), 0, ca));
     const int64_t NS = ca.GS;
     if (!c->comp_flags_fresh)  // flags only (the walked count accumulates)
         HIPCHK(c, hipMemsetAsync(c->comp_changed, 0, 16 * sizeof(unsigned int), c->stream));
@@ -312,29 +317,55 @@ static int comp_sweeps(mm_ctx *c, int n, bool resume = false) {
     return MM_OK;
 }
 
-// att at every tile start from the converged super-tile starts, then gains +
-// overlay into q2.
+// gains + overlay into q2, every tile starting from the walkers' checkpoints
 static int comp_back(mm_ctx *c) {
     const CompArgs &ca = c->ca;
-    RET(launch(c, "comp_record", comp_record_kernel, dim3(blocks_for(ca.GS, RECORD_BLOCK), 3), dim3(RECORD_BLOCK), 0, ca));
-    RET(launch(c, "comp_tstart", comp_tstart_kernel, dim3(c->comp_nb, 3), dim3(256), 0, ca));
     return launch(c, "comp_apply", comp_apply_kernel, dim3(blocks_for(ca.G, APPLY_TILES)), dim3(3 * APPLY_TILES), 0,
                   ca);
 }
 
-// Synchronises the stream; reports look-back timeouts (never expected: a block
-// only waits on blocks that started before it) and whether the queued sweeps
-// converged.
-static int chain_check(mm_ctx *c, bool *converged) {
-    unsigned e = 0, flags[16] = {0};
-    if (c->lb_error) HIPCHK(c, hipMemcpyAsync(&e, c->lb_error, 4, hipMemcpyDeviceToHost, c->stream));
+// Pinned readback block of one chain pass (offsets in bytes): look-back error
+// word, sweep flags, re-walked frame count, loudness + gain, per-chunk active counts.
+constexpr size_t RB_ERR = 0, RB_FLAGS = 16, RB_WALKED = 80, RB_LG = 96, RB_TOTALS = 128;
+
+static int ensure_rb(mm_ctx *c, size_t bytes) {
+    if (c->rb_cap >= bytes) return MM_OK;
+    if (c->rb) HIPCHK(c, hipHostFree(c->rb));
+    c->rb = nullptr;
+    c->rb_cap = 0;
+    HIPCHK(c, hipHostMalloc((void **)&c->rb, bytes, hipHostMallocDefault));
+    c->rb_cap = bytes;
+    return MM_OK;
+}
+
+static int64_t comp_chunks(const mm_ctx *c) { return c->comp_on ? c->ca.GS / c->ca.SPC : 0; }
+
+// Queue the D2H copies of everything the host checks after the chain (no sync).
+static int queue_readback(mm_ctx *c, bool lufs) {
+    const int64_t nch = comp_chunks(c);
+    RET(ensure_rb(c, RB_TOTALS + (size_t)12 * nch + 64));
+    char *rb = c->rb;
+    *reinterpret_cast<unsigned *>(rb + RB_ERR) = 0u;
+    if (c->lb_error) HIPCHK(c, hipMemcpyAsync(rb + RB_ERR, c->lb_error, 4, hipMemcpyDeviceToHost, c->stream));
     if (c->comp_on && c->comp_pending)
-        HIPCHK(c, hipMemcpyAsync(flags, c->comp_changed, c->comp_pending * sizeof(unsigned), hipMemcpyDeviceToHost,
-                                 c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (e) return set_err(c, MM_ERR_STATE, "IIR look-back timed out");
+        HIPCHK(c, hipMemcpyAsync(rb + RB_FLAGS, c->comp_changed, c->comp_pending * sizeof(unsigned),
+                                 hipMemcpyDeviceToHost, c->stream));
+    if (lufs && c->gate_out) HIPCHK(c, hipMemcpyAsync(rb + RB_LG, c->gate_out, 16, hipMemcpyDeviceToHost, c->stream));
+    if (c->comp_on) {
+        HIPCHK(c, hipMemcpyAsync(rb + RB_TOTALS, c->ca.total[0], (size_t)12 * nch, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(rb + RB_WALKED, c->ca.walked, 8, hipMemcpyDeviceToHost, c->stream));
+    }
+    return MM_OK;
+}
+
+// After the stream has drained: reports look-back timeouts (never expected: a
+// block only waits on blocks that started before it) and whether the queued
+// sweeps converged.
+static int evaluate_chain(mm_ctx *c, bool *converged) {
+    if (*reinterpret_cast<const unsigned *>(c->rb + RB_ERR)) return set_err(c, MM_ERR_STATE, "IIR look-back timed out");
     *converged = true;
     if (c->comp_on && c->comp_pending) {
+        const unsigned *flags = reinterpret_cast<const unsigned *>(c->rb + RB_FLAGS);
         int k = 0;
         while (k < c->comp_pending && flags[k]) ++k;
         c->comp_iters += k;
@@ -344,6 +375,12 @@ static int chain_check(mm_ctx *c, bool *converged) {
             return set_err(c, MM_ERR_STATE, "compressor did not converge in %d sweeps", c->comp_iters);
     }
     return MM_OK;
+}
+
+static int chain_check(mm_ctx *c, bool *converged) {
+    RET(queue_readback(c, false));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return evaluate_chain(c, converged);
 }
 
 // ------------------------------------------------------------ chain A..C
@@ -390,6 +427,7 @@ static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
     ea.width = j->width;
     ea.width_on = j->width_on && ch == 2;
     ea.q_out = reinterpret_cast<int16_t *>(q1);
+    if (j->eq.nsec > 0) RET(get_buf(c, "eq_xs", (size_t)TG * 2, &ea.xs));
     if (G > 0) {
         // --- stage A: saturation -> EQ -> width -> int16 (AME:55-63)
         if (j->eq.nsec == 0) {
@@ -419,6 +457,14 @@ static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
         fill_sos(xa.sos, j->xover, 4);
         xa.q_in = reinterpret_cast<const int16_t *>(q1);
         for (int b = 0; b < 3; ++b) xa.band[b] = reinterpret_cast<int16_t *>(bands[b]);
+        double *tile_e;  // [3][E, tail][G]
+        RET(get_buf(c, "comp_tile_e", (size_t)6 * G, &tile_e));
+        for (int b = 0; b < 3; ++b) {
+            xa.E[b] = tile_e + (size_t)(2 * b) * G;
+            xa.tail[b] = tile_e + (size_t)(2 * b + 1) * G;
+            const int r = j->band[b].look % T;
+            xa.tail_from[b] = r ? T - r : T;
+        }
         LbArgs lb{};
         RET(upload_tables(c, "xover", j->xover, lb));
         RET(lb_prepare(c, nblk, ch, lb, 1));
@@ -438,6 +484,7 @@ static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
         ca.ch = ch;
         ca.warmup = j->comp_warmup;
         ca.U = std::max(16, std::min(j->comp_super, FIX_MAX_U));
+        ca.U -= ca.U % CK_Q;
         const int64_t nchunks = (G + K - 1) / K;
         ca.SPC = ((int64_t)K * T + ca.U - 1) / ca.U;
         ca.GS = nchunks * ca.SPC;
@@ -445,11 +492,18 @@ static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
         short2 *q2;
         RET(get_buf(c, "q2", TG, &q2));
         ca.q_out = q2;
-        double *st, *eA, *eB, *tst, *luts;
+        // pass-0 ownership: enough lanes for the chip at C2 size (2 super-tiles per lane),
+        // more per lane on bigger problems and when batch streams run beside this one
+        ca.own = c->own_override > 0 ? c->own_override
+                                     : (int)std::max<int64_t>(1, std::min<int64_t>(4, (NS * c->concurrency + 3307) / 6615));
+        ca.ocols = (NS + ca.own - 1) / ca.own;
+        ca.RS = ca.ocols * ca.own;
+        const int64_t RS = ca.RS;
+        double *st, *eA, *eB, *luts, *cks;
         RET(get_buf(c, "comp_start", (size_t)3 * NS, &st));
         RET(get_buf(c, "comp_endA", (size_t)3 * NS, &eA));
         RET(get_buf(c, "comp_endB", (size_t)3 * NS, &eB));
-        RET(get_buf(c, "comp_tstart", (size_t)3 * G, &tst));
+        RET(get_buf(c, "comp_ck", (size_t)3 * RS * (ca.U / CK_Q), &cks));
         RET(get_buf(c, "comp_lut", (size_t)3 * 32769, &luts));
         unsigned int *changed = c->comp_changed;  // zeroed with the chain's control words
         ca.walked = reinterpret_cast<unsigned long long *>(changed + 32);
@@ -464,8 +518,10 @@ static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
             snprintf(nm, sizeof nm, "comp_r%d", b);
             RET(get_buf(c, nm, TG, &rb));
             snprintf(nm, sizeof nm, "comp_mc%d", b);
-            RET(get_buf(c, nm, (size_t)NS * (ca.U + 1 + WALK_PAD), &mcb));  // + compaction dummy row + walk prefetch rows
+            RET(get_buf(c, nm, (size_t)RS * (ca.U + 1 + WALK_PAD), &mcb));  // + compaction dummy row + walk prefetch rows
             ca.r16[b] = rb;
+            ca.E[b] = xa.E[b];
+            ca.tail[b] = xa.tail[b];
             ca.Mc[b] = mcb;
             ca.band[b] = bands[b];
             ca.lut[b] = luts + (size_t)b * 32769;
@@ -487,14 +543,14 @@ static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
             ca.off[b] = off + (size_t)b * G;
             ca.total[b] = tot + (size_t)b * nchunks;
             ca.start[b] = st + (size_t)b * NS;
-            ca.tstart[b] = tst + (size_t)b * G;
+            ca.ck[b] = cks + (size_t)b * RS * (ca.U / CK_Q);
             ca.end_out[b] = eA + (size_t)b * NS;
         }
         RET(launch(c, "comp_rms", comp_rms_kernel, dim3(nb, 3), dim3(256), 0, ca));
         RET(launch(c, "comp_offsets", comp_offsets_kernel, dim3((unsigned)nchunks, 3), dim3(1024), 0, ca));
         RET(launch(c, "comp_compact", comp_compact_kernel, dim3(nb, 3), dim3(256), 0, ca));
         RET(launch(c, "comp_pass0", comp_pass0_kernel,
-                   dim3(blocks_for((NS + PASS0_OWN - 1) / PASS0_OWN, PASS0_BLOCK), 3), dim3(PASS0_BLOCK), 0, ca));
+                   dim3(blocks_for((NS + ca.own - 1) / ca.own, PASS0_BLOCK), 3), dim3(PASS0_BLOCK), 0, ca));
         c->comp_on = true;
         c->ca = ca;
         c->comp_cur = eA;
@@ -673,47 +729,49 @@ static int finalize(mm_ctx *c, double gain, const double *gain_dev, int use_gain
     return launch(c, "finalize", finalize_kernel<1>, dim3(blocks_for(c->G, FIN_TILES)), dim3(256), lds, fa);
 }
 
-// The chain is queued without host round trips; one sync at the end checks
-// the compressor's convergence (a rare unconverged batch is extended and the
-// dependent stages re-run) and fetches the loudness.
-static int master_device(mm_ctx *c, const mm_job *j, const void *d_in, void *d_out, mm_result *res) {
-    RET(stage_front(c, j, d_in));
+// The chain is queued without host round trips (enqueue_chain); one sync at the
+// end (complete_chain) checks the compressor's convergence (a rare unconverged
+// batch is extended and the dependent stages re-run) and reads the loudness.
+static int enqueue_tail(mm_ctx *c, const mm_job *j, void *d_out) {
     const bool lufs = j->lufs_on && c->G > 0;
+    if (lufs) RET(kweight_device(c));
+    RET(finalize(c, 1.0, lufs ? c->gate_out + 1 : nullptr, j->lufs_on, d_out));
+    return queue_readback(c, lufs);
+}
+
+static int enqueue_chain(mm_ctx *c, const mm_job *j, const void *d_in, void *d_out) {
+    RET(stage_front(c, j, d_in));
+    return enqueue_tail(c, j, d_out);
+}
+
+static int complete_chain(mm_ctx *c, const mm_job *j, void *d_out, mm_result *res) {
     for (;;) {
-        if (lufs) RET(kweight_device(c));
-        RET(finalize(c, 1.0, lufs ? c->gate_out + 1 : nullptr, j->lufs_on, d_out));
-        double lg[2] = {NAN, 1.0};
-        if (lufs) HIPCHK(c, hipMemcpyAsync(lg, c->gate_out, sizeof lg, hipMemcpyDeviceToHost, c->stream));
-        unsigned long long walked = 0;
-        std::vector<int32_t> totals;
-        if (res && c->comp_on) {
-            const int64_t nchunks = c->ca.GS / c->ca.SPC;
-            totals.resize((size_t)3 * nchunks);
-            HIPCHK(c, hipMemcpyAsync(totals.data(), c->ca.total[0], totals.size() * 4, hipMemcpyDeviceToHost,
-                                     c->stream));
-            HIPCHK(c, hipMemcpyAsync(&walked, c->ca.walked, 8, hipMemcpyDeviceToHost, c->stream));
-        }
+        HIPCHK(c, hipStreamSynchronize(c->stream));
         bool converged;
-        RET(chain_check(c, &converged));
-        if (converged) {
-            if (j->lufs_on && c->G == 0) {  // nothing measured: pyloudnorm would have raised earlier
-                lg[0] = -INFINITY;
-                lg[1] = INFINITY;
-            }
-            if (res) {
-                res->loudness = j->lufs_on ? lg[0] : NAN;
-                res->gain_linear = j->lufs_on ? lg[1] : 1.0;
-                res->frames_out = j->frames_proc;
-                res->comp_iters = c->comp_iters;
-                res->comp_active = 0;
-                for (int32_t t : totals) res->comp_active += t;
-                res->comp_walked = (int64_t)walked;
-            }
-            return MM_OK;
-        }
-        RET(comp_sweeps(c, 8, true));
+        RET(evaluate_chain(c, &converged));
+        if (converged) break;
+        RET(comp_sweeps(c, 8));
         RET(comp_back(c));
+        RET(enqueue_tail(c, j, d_out));
     }
+    if (res) {
+        const bool lufs = j->lufs_on && c->G > 0;
+        const double *lg = reinterpret_cast<const double *>(c->rb + RB_LG);
+        res->loudness = j->lufs_on ? (lufs ? lg[0] : -INFINITY) : NAN;  // no frames: pyloudnorm raised earlier
+        res->gain_linear = j->lufs_on ? (lufs ? lg[1] : INFINITY) : 1.0;
+        res->frames_out = j->frames_proc;
+        res->comp_iters = c->comp_iters;
+        res->comp_active = 0;
+        const int32_t *tot = reinterpret_cast<const int32_t *>(c->rb + RB_TOTALS);
+        for (int64_t k = 0; k < 3 * comp_chunks(c); ++k) res->comp_active += tot[k];
+        res->comp_walked = c->comp_on ? (int64_t) * reinterpret_cast<const unsigned long long *>(c->rb + RB_WALKED) : 0;
+    }
+    return MM_OK;
+}
+
+static int master_device(mm_ctx *c, const mm_job *j, const void *d_in, void *d_out, mm_result *res) {
+    RET(enqueue_chain(c, j, d_in, d_out));
+    return complete_chain(c, j, d_out, res);
 }
 
 // Stage the chunk chain of a range (time-sharded ranks) to convergence.
@@ -723,7 +781,7 @@ static int stage_chunks(mm_ctx *c, const mm_job *j, const void *d_in) {
         bool converged;
         RET(chain_check(c, &converged));
         if (converged) return MM_OK;
-        RET(comp_sweeps(c, 8, true));
+        RET(comp_sweeps(c, 8));
         RET(comp_back(c));
     }
 }
@@ -742,6 +800,7 @@ int mm_create(int device, mm_ctx **out) {
         delete c;
         return MM_ERR_HIP;
     }
+    if (const char *o = getenv("MM_PASS0_OWN")) c->own_override = std::max(0, std::min(8, atoi(o)));
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return MM_ERR_HIP;
@@ -763,6 +822,8 @@ int mm_destroy(mm_ctx *c) {
         if (c->pin[b]) hipHostFree(c->pin[b]);
         if (c->pin_ev[b]) hipEventDestroy(c->pin_ev[b]);
     }
+    if (c->rb) hipHostFree(c->rb);
+    for (mm_ctx *k : c->children) mm_destroy(k);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
     return MM_OK;
@@ -781,6 +842,70 @@ int mm_master_device(mm_ctx *c, const mm_job *j, const void *d_in, void *d_out, 
     if (!c) return MM_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
     return master_device(c, j, d_in, d_out, res);
+}
+
+// A batch of independent tracks (BASELINE C3/C5 on one GPU): job i runs on child
+// context i % S (own stream and buffers, S = min(n, MM_BATCH_STREAMS)), so the
+// chains of up to S tracks are in flight at once and their latency-bound kernels
+// fill each other's idle SIMDs.  Jobs are completed in submission order; a
+// child's next job is queued as soon as its previous one has been checked.
+int mm_master_batch(mm_ctx *c, int n, const mm_job *jobs, const void *const *d_in, void *const *d_out,
+                    mm_result *res) {
+    if (!c || n < 0 || (n > 0 && (!jobs || !d_in || !d_out))) return set_err(c, MM_ERR_ARG, "bad arguments");
+    HIPCHK(c, hipSetDevice(c->device));
+    for (int i = 0; i < n; ++i) RET(validate(c, &jobs[i]));
+    const int S = std::min(n, MM_BATCH_STREAMS);
+    while ((int)c->children.size() < S) {
+        mm_ctx *k = nullptr;
+        if (mm_create(c->device, &k) != MM_OK) return set_err(c, MM_ERR_HIP, "cannot create a batch stream");
+        c->children.push_back(k);
+    }
+    for (int s = 0; s < S; ++s) {
+        c->children[s]->timing = c->timing;
+        c->children[s]->concurrency = S;
+    }
+    std::vector<int> cur((size_t)S, -1);
+    int next = 0;
+    auto fail = [&](mm_ctx *k) {
+        set_err(c, MM_ERR_STATE, "batch job: %s", k->err);
+        for (int s = 0; s < S; ++s) hipStreamSynchronize(c->children[s]->stream);
+        return MM_ERR_STATE;
+    };
+    for (int s = 0; s < S && next < n; ++s, ++next) {
+        cur[s] = next;
+        if (enqueue_chain(c->children[s], &jobs[next], d_in[next], d_out[next]) != MM_OK) return fail(c->children[s]);
+    }
+    for (int done = 0; done < n;) {
+        for (int s = 0; s < S; ++s) {
+            if (cur[s] < 0) continue;
+            mm_ctx *k = c->children[s];
+            const int i = cur[s];
+            if (complete_chain(k, &jobs[i], d_out[i], res ? &res[i] : nullptr) != MM_OK) return fail(k);
+            ++done;
+            cur[s] = -1;
+            if (next < n) {
+                cur[s] = next;
+                if (enqueue_chain(k, &jobs[next], d_in[next], d_out[next]) != MM_OK) return fail(k);
+                ++next;
+            }
+        }
+    }
+    for (int s = 0; s < S; ++s) {  // per-kernel timing of the children lands in the parent's stats
+        mm_ctx *k = c->children[s];
+        resolve_events(k);
+        for (auto &nm : k->stat_order) {
+            auto it = c->stats.find(nm);
+            if (it == c->stats.end()) {
+                c->stat_order.push_back(nm);
+                it = c->stats.emplace(nm, KStat{}).first;
+            }
+            it->second.ms += k->stats[nm].ms;
+            it->second.n += k->stats[nm].n;
+        }
+        k->stats.clear();
+        k->stat_order.clear();
+    }
+    return MM_OK;
 }
 
 int mm_master(mm_ctx *c, const mm_job *j, const void *in, void *out, mm_result *res) {

@@ -31,8 +31,15 @@ EQ_PRESETS = {
 
 COMP_WARMUP = int(os.environ.get("MM_COMP_WARMUP", "6"))  # super-tiles of warm-up walk before each one
 COMP_MAX_ITERS = 100000
-# envelope solve unit (active frames) -> ~8 Jacobi sweeps on pink noise; MM_COMP_SUPER overrides
+# envelope solve unit in active frames at 44.1 kHz (MM_COMP_SUPER overrides).  The
+# envelope's time constants are in ms (attack/release frames scale with the rate),
+# so the trajectories' coalescence lengths scale with the rate too: the unit does.
 COMP_SUPER_FRAMES = int(os.environ.get("MM_COMP_SUPER", "1000"))
+
+
+def comp_super_frames(rate: int) -> int:
+    """Super-tile length (active frames, a multiple of 8) for `rate`."""
+    return max(64, int(round(COMP_SUPER_FRAMES * rate / 44100 / 8)) * 8)
 
 
 class Job:
@@ -108,7 +115,7 @@ class Job:
                 jb.lut = tab.ctypes.data_as(native.c_double_p)
         j.comp_warmup = COMP_WARMUP
         j.comp_max_iters = COMP_MAX_ITERS
-        j.comp_super = COMP_SUPER_FRAMES
+        j.comp_super = comp_super_frames(self.rate)
         # --- loudness
         if lufs is not None:
             self._fill_iir(j.kweight, design.kweight_sections(self.rate), [2], self.tile, design.LB_THREADS)
@@ -199,6 +206,19 @@ def master_device(ctx: native.Context, job: Job, d_in: int, d_out: int, res: nat
                                        ctypes.c_void_p(d_out), ctypes.byref(res) if res is not None else None),
               "mm_master_device")
     return res
+
+
+def master_batch(ctx: native.Context, jobs, d_ins, d_outs, with_results: bool = True):
+    """A batch of independent tracks with device-resident inputs/outputs
+    (mm_master_batch): up to native.BATCH_STREAMS of them in flight at once, each on
+    its own stream.  Returns one MMResult per job (or None)."""
+    n = len(jobs)
+    arr = (native.MMJob * n)(*[j.job for j in jobs])
+    ins = (ctypes.c_void_p * n)(*[ctypes.c_void_p(int(p)) for p in d_ins])
+    outs = (ctypes.c_void_p * n)(*[ctypes.c_void_p(int(p)) for p in d_outs])
+    res = (native.MMResult * n)() if with_results else None
+    ctx.check(ctx.lib.mm_master_batch(ctx.ptr, n, arr, ins, outs, res), "mm_master_batch")
+    return list(res) if with_results else None
 
 
 def process(input_path: str, output_path: str, params: dict, device: int = 0, verbose: bool = False) -> dict:

@@ -18,6 +18,7 @@ MM_OUT_I16, MM_OUT_F32 = 0, 1
 MM_IN_F32, MM_IN_I16 = 0, 1
 MM_F32, MM_F64 = 0, 1  # per-stage operator sample dtypes
 MM_ERR_ARG = -1
+BATCH_STREAMS = 8  # MM_BATCH_STREAMS
 MAX_DIM, TILE_POW, BLK_POW = 8, 8, 65
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
@@ -68,7 +69,7 @@ EXPORTS = ("mm_create", "mm_destroy", "mm_last_error", "mm_sync", "mm_version", 
            "mm_read_mix", "mm_timing", "mm_kernel_stats", "mm_comm_unique_id", "mm_comm_init", "mm_comm_destroy",
            "mm_allreduce_sum_f64", "mm_allgather_f64", "mm_wav_probe", "mm_master_wav",
            "mm_op_pcm_to_float", "mm_op_saturation", "mm_op_stereo_width", "mm_op_quantize", "mm_op_soft_limiter",
-           "mm_op_gain", "mm_op_sosfilt", "mm_op_loudness", "mm_op_multiband")
+           "mm_op_gain", "mm_op_sosfilt", "mm_op_loudness", "mm_op_multiband", "mm_master_batch")
 
 _lib = None
 _lock = threading.Lock()
@@ -97,6 +98,7 @@ def load():
             "mm_version": ([], ctypes.c_int),
             "mm_master": ([vp, P(MMJob), vp, vp, P(MMResult)], ctypes.c_int),
             "mm_master_device": ([vp, P(MMJob), vp, vp, P(MMResult)], ctypes.c_int),
+            "mm_master_batch": ([vp, ctypes.c_int, P(MMJob), P(vp), P(vp), P(MMResult)], ctypes.c_int),
             "mm_stage_chunks": ([vp, P(MMJob), vp], ctypes.c_int),
             "mm_wav_probe": ([vp, ctypes.c_char_p, P(MMWavInfo)], ctypes.c_int),
             "mm_master_wav": ([vp, P(MMJob), ctypes.c_char_p, ctypes.c_char_p, P(MMResult)], ctypes.c_int),

@@ -37,3 +37,16 @@ def pink_noise_pcm16(frames: int, rate: int = 44100, channels: int = 2, track: i
         y = x * (target / rms if rms > 0 else 0.0)
         out[:, c] = np.clip(np.round(y * 32768.0), -32768, 32767).astype(np.int16)
     return out[:, 0] if channels == 1 else out
+
+
+def pink_noise_chunks(c0: int, c1: int, rate: int = 44100, channels: int = 2, track: int = 0,
+                      level_dbfs: float = -18.0, chunk_s: int = 30) -> np.ndarray:
+    """Frames of 30 s chunks [c0, c1) of a long synthetic track, each chunk its own
+    pink-noise block (seeded by track and chunk index, scaled to `level_dbfs`), so a
+    time-sharded rank (BASELINE C4: 2 h = 240 chunks) generates only its own range."""
+    n = chunk_s * rate
+    out = np.empty(((c1 - c0) * n, channels) if channels > 1 else ((c1 - c0) * n,), np.int16)
+    for k, c in enumerate(range(c0, c1)):
+        out[k * n:(k + 1) * n] = pink_noise_pcm16(n, rate, channels, track=100003 * (track + 1) + c,
+                                                  level_dbfs=level_dbfs)
+    return out

@@ -63,14 +63,14 @@ __global__ void __launch_bounds__(64) walk(const double *M, int n, C c, double *
 }
 // rms code r (uint16, 2 B/step from HBM) + L2-resident table gathers: G == 1
 // gathers M and divides inline; G == 2 gathers {M, M/A, M/R, 0} (32 B rows)
-template <int G>
+template <int G, int L = 8>
 __global__ void __launch_bounds__(64) walk_r(const uint16_t *Rc, const double *lut, const double4 *lut4, int n, C c,
                                              double *out, long long *cyc) {
     const int lane = threadIdx.x + blockIdx.x * 64;
     const uint16_t *p = Rc + lane;
     const int S = gridDim.x * 64;
     double att = 0.0;
-    constexpr int B = 32, L = 8;  // r prefetched B ahead, table rows L ahead
+    constexpr int B = 32;  // r prefetched B ahead, table rows L ahead
     uint16_t rb[B];
 #pragma unroll
     for (int k = 0; k < B; ++k) rb[k] = p[(long)k * S];
@@ -105,13 +105,13 @@ __global__ void __launch_bounds__(64) walk_r(const uint16_t *Rc, const double *l
     out[lane] = att;
     if (lane == 0) cyc[0] = t1 - t0;
 }
-template <int G>
+template <int G, int L = 8>
 void run_r(const char *name, const uint16_t *R, const double *lut, const double4 *lut4, int n, double *o, long long *cy, int blocks) {
     C c{441.0, 1.0 / 441.0, 8820.0, 1.0 / 8820.0};
     hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
-    walk_r<G><<<blocks, 64>>>(R, lut, lut4, n, c, o, cy);
+    walk_r<G, L><<<blocks, 64>>>(R, lut, lut4, n, c, o, cy);
     (void)hipEventRecord(e0);
-    walk_r<G><<<blocks, 64>>>(R, lut, lut4, n, c, o, cy);
+    walk_r<G, L><<<blocks, 64>>>(R, lut, lut4, n, c, o, cy);
     (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
     float ms; (void)hipEventElapsedTime(&ms, e0, e1);
     long long h; (void)hipMemcpy(&h, cy, 8, hipMemcpyDeviceToHost);
@@ -152,9 +152,11 @@ int main() {
         for (int r = 0; r < 32769; ++r) { h[4*r] = r * 1e-3; h[4*r+1] = h[4*r] / 441.0; h[4*r+2] = h[4*r] / 8820.0; h[4*r+3] = 0; }
         (void)hipMemcpy(lut4, h, 32769 * 32, hipMemcpyHostToDevice);
     }
-    for (int blocks : {414, 1024}) {
+    for (int blocks : {312, 1024}) {  // <= maxb (the buffers hold maxb blocks)
         run_r<1>("r16 + gather M, divide", R, lut, lut4, n, o, cy, blocks);
         run_r<2>("r16 + gather {M,M/A,M/R}", R, lut, lut4, n, o, cy, blocks);
+        run_r<2, 16>("r16 + gather rows, 16 ahead", R, lut, lut4, n, o, cy, blocks);
+        run_r<2, 24>("r16 + gather rows, 24 ahead", R, lut, lut4, n, o, cy, blocks);
         run<0, 1>("inline divisions (current)", M, n, o, cy, blocks);
         run<1, 2>("divisions 2 frames ahead", M, n, o, cy, blocks);
         run<1, 4>("divisions 4 frames ahead", M, n, o, cy, blocks);
