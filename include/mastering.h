@@ -219,6 +219,19 @@ int mm_op_sosfilt(mm_ctx *ctx, int dtype, const void *in, int64_t frames, int ch
  * job: channels, frames_proc, kweight (tpb 256), loudness geometry, lufs_target.
  * out[0] = loudness (LUFS), out[1] = 10 ** ((lufs_target - L) / 20). */
 int mm_op_loudness(mm_ctx *ctx, const mm_job *job, int dtype, const void *in, double *out);
+/* The legacy engine's variants (main.py:94-192, mastering_amd/legacy.py):
+ * saturation tanh(x*g)/g with g = 1 + 4*amount/100 (main.py:94-97); limiter
+ * |x| > threshold -> tanh(x)*threshold (main.py:189-192); an EQ stage as the
+ * parallel mix a*x + c*sosfilt(x) of its butter() filter (main.py:133-154: the
+ * a*x product in f32 for f32 samples, numpy's rule), f64 out; and the compressor
+ * + overlay on three given int16 band arrays (main.py:156-177, whose mid band is
+ * LP4000(HP250(x)) rather than x - lo - hi). */
+int mm_op_saturation_legacy(mm_ctx *ctx, int dtype, const void *in, int64_t n, double amount, void *out);
+int mm_op_soft_limiter_legacy(mm_ctx *ctx, int dtype, void *inout, int64_t n, double threshold);
+int mm_op_sosfilt_mix(mm_ctx *ctx, int dtype, const void *in, int64_t frames, int channels, const mm_iir *f,
+                      double a, double c, double *out);
+int mm_op_compress_bands(mm_ctx *ctx, const mm_job *job, const int16_t *lo, const int16_t *mid, const int16_t *hi,
+                         int16_t *out);
 /* apply_multiband_compressor (AME:196-210) on int16 PCM [frames][channels]:
  * job with multiband_on, in_kind MM_IN_I16, EQ/exciter/width/loudness off and one
  * chunk covering the input (tile * tiles_per_chunk >= frames_proc); out has the

@@ -383,6 +383,124 @@ static int chain_check(mm_ctx *c, bool *converged) {
     return evaluate_chain(c, converged);
 }
 
+// Control words of the whole chain, zeroed by ONE memset: [0] look-back error,
+// [256..512) sweep flags + walked count, then the eq / crossover / K-weighting
+// look-back regions (each fresh until its first use).
+static int setup_control(mm_ctx *c, unsigned nblk) {
+    const size_t region = lb_flag_bytes(nblk);  // >= the K-weighting stage's (256 tiles per block)
+    const size_t bytes = 512 + 3 * region;
+    char *ctl;
+    RET(get_buf(c, "ctl", bytes, &ctl));
+    HIPCHK(c, hipMemsetAsync(ctl, 0, bytes, c->stream));
+    c->lb_error = reinterpret_cast<unsigned *>(ctl);
+    c->comp_changed = reinterpret_cast<unsigned *>(ctl + 256);
+    for (int r = 0; r < 3; ++r) {
+        c->ctl_lb[r] = reinterpret_cast<unsigned *>(ctl + 512 + r * region);
+        c->ctl_fresh[r] = true;
+    }
+    c->comp_flags_fresh = true;
+    return MM_OK;
+}
+
+// Stage C (AME:207-210): per-band pydub compressor envelope solve + gains +
+// overlay of the three int16 band planes (tile-major) into q2.  tile_e holds the
+// crossover's per-tile band energies ([3][E, tail][G]).  Queues everything up to
+// the apply; convergence is checked at the chain's sync.
+static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], const double *tile_e, short2 **q2_out) {
+    const int T = j->tile, ch = j->channels, K = j->tiles_per_chunk;
+    const int64_t N = j->frames_proc;
+    const int64_t G = c->G;
+    const int64_t TG = (int64_t)T * std::max<int64_t>(G, 1);
+    const unsigned nb = blocks_for(std::max<int64_t>(G, 1), 256);
+    CompArgs ca{};
+    ca.N_proc = N;
+    ca.G = G;
+    ca.T = T;
+    ca.K = K;
+    ca.ch = ch;
+    ca.warmup = j->comp_warmup;
+    ca.U = std::max(16, std::min(j->comp_super, FIX_MAX_U));
+    ca.U -= ca.U % CK_Q;
+    const int64_t nchunks = (G + K - 1) / K;
+    ca.SPC = ((int64_t)K * T + ca.U - 1) / ca.U;
+    ca.GS = nchunks * ca.SPC;
+    const int64_t NS = ca.GS;
+    short2 *q2;
+    RET(get_buf(c, "q2", TG, &q2));
+    ca.q_out = q2;
+    *q2_out = q2;
+    // pass-0 ownership: enough lanes for the chip at C2 size (2 super-tiles per lane),
+    // more per lane on bigger problems and when batch streams run beside this one
+    ca.own = c->own_override > 0 ? c->own_override
+                                 : (int)std::max<int64_t>(1, std::min<int64_t>(4, (NS * c->concurrency + 3307) / 6615));
+    ca.ocols = (NS + ca.own - 1) / ca.own;
+    ca.RS = ca.ocols * ca.own;
+    const int64_t RS = ca.RS;
+    double *st, *eA, *eB, *luts, *cks;
+    RET(get_buf(c, "comp_start", (size_t)3 * NS, &st));
+    RET(get_buf(c, "comp_endA", (size_t)3 * NS, &eA));
+    RET(get_buf(c, "comp_endB", (size_t)3 * NS, &eB));
+    RET(get_buf(c, "comp_ck", (size_t)3 * RS * (ca.U / CK_Q), &cks));
+    RET(get_buf(c, "comp_lut", (size_t)3 * 32769, &luts));
+    unsigned int *changed = c->comp_changed;  // zeroed with the chain's control words
+    ca.walked = reinterpret_cast<unsigned long long *>(changed + 32);
+    int32_t *cnt, *off, *tot;
+    RET(get_buf(c, "comp_cnt", (size_t)3 * G, &cnt));
+    RET(get_buf(c, "comp_off", (size_t)3 * G, &off));
+    RET(get_buf(c, "comp_total", (size_t)3 * nchunks, &tot));
+    for (int b = 0; b < 3; ++b) {
+        uint16_t *rb;
+        double *mcb;
+        char nm[16];
+        snprintf(nm, sizeof nm, "comp_r%d", b);
+        RET(get_buf(c, nm, TG, &rb));
+        snprintf(nm, sizeof nm, "comp_mc%d", b);
+        RET(get_buf(c, nm, (size_t)RS * (ca.U + 1 + WALK_PAD), &mcb));  // + compaction dummy row + walk prefetch rows
+        ca.r16[b] = rb;
+        ca.E[b] = tile_e + (size_t)(2 * b) * G;
+        ca.tail[b] = tile_e + (size_t)(2 * b + 1) * G;
+        ca.Mc[b] = mcb;
+        ca.band[b] = bands[b];
+        ca.lut[b] = luts + (size_t)b * 32769;
+        // tables are immutable host arrays owned by the caller's job: upload once
+        if (c->lut_src[b] != j->band[b].lut) {
+            // the M column of the host's {M, M/A, M/R, 0} rows
+            HIPCHK(c, hipMemcpy2DAsync(luts + (size_t)b * 32769, sizeof(double), j->band[b].lut,
+                                       4 * sizeof(double), sizeof(double), 32769, hipMemcpyHostToDevice,
+                                       c->stream));
+            c->lut_src[b] = j->band[b].lut;
+        }
+        ca.r0[b] = (uint32_t)j->band[b].r0;
+        ca.look[b] = j->band[b].look;
+        ca.attack_frames[b] = j->band[b].attack_frames;
+        ca.release_frames[b] = j->band[b].release_frames;
+        ca.rcp_attack[b] = 1.0 / j->band[b].attack_frames;
+        ca.rcp_release[b] = 1.0 / j->band[b].release_frames;
+        ca.cnt[b] = cnt + (size_t)b * G;
+        ca.off[b] = off + (size_t)b * G;
+        ca.total[b] = tot + (size_t)b * nchunks;
+        ca.start[b] = st + (size_t)b * NS;
+        ca.ck[b] = cks + (size_t)b * RS * (ca.U / CK_Q);
+        ca.end_out[b] = eA + (size_t)b * NS;
+    }
+    RET(launch(c, "comp_rms", comp_rms_kernel, dim3(nb, 3), dim3(256), 0, ca));
+    RET(launch(c, "comp_offsets", comp_offsets_kernel, dim3((unsigned)nchunks, 3), dim3(1024), 0, ca));
+    RET(launch(c, "comp_compact", comp_compact_kernel, dim3(nb, 3), dim3(256), 0, ca));
+    RET(launch(c, "comp_pass0", comp_pass0_kernel,
+               dim3(blocks_for((NS + ca.own - 1) / ca.own, PASS0_BLOCK), 3), dim3(PASS0_BLOCK), 0, ca));
+    c->comp_on = true;
+    c->ca = ca;
+    c->comp_cur = eA;
+    c->comp_nxt = eB;
+    c->comp_changed = changed;
+    c->comp_iters = 0;
+    c->comp_pending = 0;
+    c->comp_nb = nb;
+    RET(comp_sweeps(c, COMP_SWEEPS));
+    RET(comp_back(c));
+    return MM_OK;
+}
+
 // ------------------------------------------------------------ chain A..C
 static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
     RET(validate(c, j));
@@ -397,21 +515,7 @@ static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
     RET(get_buf(c, "q1", TG, &q1));
     const int tpb = LB_THREADS / ch;
     const unsigned nblk = blocks_for(std::max<int64_t>(G, 1), tpb);
-    {  // control words of the whole chain: [0] look-back error, [64..128) sweep
-       // flags + walked count, then the eq / crossover / K-weighting regions
-        const size_t region = lb_flag_bytes(nblk);  // >= the K-weighting stage's (256 tiles per block)
-        const size_t bytes = 512 + 3 * region;
-        char *ctl;
-        RET(get_buf(c, "ctl", bytes, &ctl));
-        HIPCHK(c, hipMemsetAsync(ctl, 0, bytes, c->stream));
-        c->lb_error = reinterpret_cast<unsigned *>(ctl);
-        c->comp_changed = reinterpret_cast<unsigned *>(ctl + 256);
-        for (int r = 0; r < 3; ++r) {
-            c->ctl_lb[r] = reinterpret_cast<unsigned *>(ctl + 512 + r * region);
-            c->ctl_fresh[r] = true;
-        }
-        c->comp_flags_fresh = true;
-    }
+    RET(setup_control(c, nblk));
 
     EqArgs ea{};
     ea.in = j->in_kind == MM_IN_I16 ? nullptr : static_cast<const float *>(d_in);
@@ -476,91 +580,8 @@ static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
                        (int64_t)K));
 
         // --- stage C: 3-band compressor + overlay (AME:207-210)
-        CompArgs ca{};
-        ca.N_proc = N;
-        ca.G = G;
-        ca.T = T;
-        ca.K = K;
-        ca.ch = ch;
-        ca.warmup = j->comp_warmup;
-        ca.U = std::max(16, std::min(j->comp_super, FIX_MAX_U));
-        ca.U -= ca.U % CK_Q;
-        const int64_t nchunks = (G + K - 1) / K;
-        ca.SPC = ((int64_t)K * T + ca.U - 1) / ca.U;
-        ca.GS = nchunks * ca.SPC;
-        const int64_t NS = ca.GS;
         short2 *q2;
-        RET(get_buf(c, "q2", TG, &q2));
-        ca.q_out = q2;
-        // pass-0 ownership: enough lanes for the chip at C2 size (2 super-tiles per lane),
-        // more per lane on bigger problems and when batch streams run beside this one
-        ca.own = c->own_override > 0 ? c->own_override
-                                     : (int)std::max<int64_t>(1, std::min<int64_t>(4, (NS * c->concurrency + 3307) / 6615));
-        ca.ocols = (NS + ca.own - 1) / ca.own;
-        ca.RS = ca.ocols * ca.own;
-        const int64_t RS = ca.RS;
-        double *st, *eA, *eB, *luts, *cks;
-        RET(get_buf(c, "comp_start", (size_t)3 * NS, &st));
-        RET(get_buf(c, "comp_endA", (size_t)3 * NS, &eA));
-        RET(get_buf(c, "comp_endB", (size_t)3 * NS, &eB));
-        RET(get_buf(c, "comp_ck", (size_t)3 * RS * (ca.U / CK_Q), &cks));
-        RET(get_buf(c, "comp_lut", (size_t)3 * 32769, &luts));
-        unsigned int *changed = c->comp_changed;  // zeroed with the chain's control words
-        ca.walked = reinterpret_cast<unsigned long long *>(changed + 32);
-        int32_t *cnt, *off, *tot;
-        RET(get_buf(c, "comp_cnt", (size_t)3 * G, &cnt));
-        RET(get_buf(c, "comp_off", (size_t)3 * G, &off));
-        RET(get_buf(c, "comp_total", (size_t)3 * nchunks, &tot));
-        for (int b = 0; b < 3; ++b) {
-            uint16_t *rb;
-            double *mcb;
-            char nm[16];
-            snprintf(nm, sizeof nm, "comp_r%d", b);
-            RET(get_buf(c, nm, TG, &rb));
-            snprintf(nm, sizeof nm, "comp_mc%d", b);
-            RET(get_buf(c, nm, (size_t)RS * (ca.U + 1 + WALK_PAD), &mcb));  // + compaction dummy row + walk prefetch rows
-            ca.r16[b] = rb;
-            ca.E[b] = xa.E[b];
-            ca.tail[b] = xa.tail[b];
-            ca.Mc[b] = mcb;
-            ca.band[b] = bands[b];
-            ca.lut[b] = luts + (size_t)b * 32769;
-            // tables are immutable host arrays owned by the caller's job: upload once
-            if (c->lut_src[b] != j->band[b].lut) {
-                // the M column of the host's {M, M/A, M/R, 0} rows
-                HIPCHK(c, hipMemcpy2DAsync(luts + (size_t)b * 32769, sizeof(double), j->band[b].lut,
-                                           4 * sizeof(double), sizeof(double), 32769, hipMemcpyHostToDevice,
-                                           c->stream));
-                c->lut_src[b] = j->band[b].lut;
-            }
-            ca.r0[b] = (uint32_t)j->band[b].r0;
-            ca.look[b] = j->band[b].look;
-            ca.attack_frames[b] = j->band[b].attack_frames;
-            ca.release_frames[b] = j->band[b].release_frames;
-            ca.rcp_attack[b] = 1.0 / j->band[b].attack_frames;
-            ca.rcp_release[b] = 1.0 / j->band[b].release_frames;
-            ca.cnt[b] = cnt + (size_t)b * G;
-            ca.off[b] = off + (size_t)b * G;
-            ca.total[b] = tot + (size_t)b * nchunks;
-            ca.start[b] = st + (size_t)b * NS;
-            ca.ck[b] = cks + (size_t)b * RS * (ca.U / CK_Q);
-            ca.end_out[b] = eA + (size_t)b * NS;
-        }
-        RET(launch(c, "comp_rms", comp_rms_kernel, dim3(nb, 3), dim3(256), 0, ca));
-        RET(launch(c, "comp_offsets", comp_offsets_kernel, dim3((unsigned)nchunks, 3), dim3(1024), 0, ca));
-        RET(launch(c, "comp_compact", comp_compact_kernel, dim3(nb, 3), dim3(256), 0, ca));
-        RET(launch(c, "comp_pass0", comp_pass0_kernel,
-                   dim3(blocks_for((NS + ca.own - 1) / ca.own, PASS0_BLOCK), 3), dim3(PASS0_BLOCK), 0, ca));
-        c->comp_on = true;
-        c->ca = ca;
-        c->comp_cur = eA;
-        c->comp_nxt = eB;
-        c->comp_changed = changed;
-        c->comp_iters = 0;
-        c->comp_pending = 0;
-        c->comp_nb = nb;
-        RET(comp_sweeps(c, COMP_SWEEPS));
-        RET(comp_back(c));
+        RET(stage_compress(c, j, bands, tile_e, &q2));
         mix = q2;
     } else {
         c->comp_on = false;

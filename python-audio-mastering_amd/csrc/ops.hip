@@ -13,7 +13,7 @@
 
 namespace mm {
 
-enum PwOp { PW_PCM16, PW_SAT, PW_WIDTH, PW_QUANT, PW_LIMIT, PW_GAIN, PW_MONO };
+enum PwOp { PW_PCM16, PW_SAT, PW_WIDTH, PW_QUANT, PW_LIMIT, PW_GAIN, PW_MONO, PW_SAT_LEGACY, PW_LIMIT_LEGACY };
 
 struct PwArgs {
     int64_t n;        // elements (frames for WIDTH / MONO)
@@ -92,6 +92,20 @@ __global__ void __launch_bounds__(256) pointwise_kernel(PwArgs a) {
             static_cast<T *>(a.out)[i] = limit_op<T>(static_cast<const T *>(a.in)[i], a.p0);
         } else if constexpr (OP == PW_GAIN) {  // samples * np.float64 gain -> f64 (AME:222)
             static_cast<double *>(a.out)[i] = __dmul_rn((double)static_cast<const T *>(a.in)[i], a.p0);
+        } else if constexpr (OP == PW_SAT_LEGACY) {  // legacy main.py:94-97: tanh(x * g) / g, g = 1 + 4 s / 100
+            const T x = static_cast<const T *>(a.in)[i];
+            if constexpr (sizeof(T) == 4)
+                static_cast<T *>(a.out)[i] = __fdiv_rn(tanhf(__fmul_rn(x, (float)a.p0)), (float)a.p0);
+            else
+                static_cast<T *>(a.out)[i] = __ddiv_rn(tanh(__dmul_rn(x, a.p0)), a.p0);
+        } else if constexpr (OP == PW_LIMIT_LEGACY) {  // legacy main.py:189-192: |x| > thr -> tanh(x) * thr
+            T y = static_cast<const T *>(a.in)[i];
+            if constexpr (sizeof(T) == 4) {
+                if (fabsf(y) > (float)a.p0) y = __fmul_rn(tanhf(y), (float)a.p0);
+            } else {
+                if (fabs(y) > a.p0) y = __dmul_rn(tanh(y), a.p0);
+            }
+            static_cast<T *>(a.out)[i] = y;
         } else if constexpr (OP == PW_MONO) {  // samples.mean(axis=1) (AME:215), in T
             const T *x = static_cast<const T *>(a.in) + 2 * i;
             if constexpr (sizeof(T) == 4) static_cast<T *>(a.out)[i] = __fdiv_rn(__fadd_rn(x[0], x[1]), 2.0f);
@@ -159,6 +173,10 @@ struct IirOpArgs {
     double sos[4][5];
     const double *in;  // tile-major
     double *out;       // tile-major (may alias in: every lane reads its frame before writing it)
+    // optional parallel mix of the legacy engine's EQ stages (main.py:133-154):
+    // out = a * x + c * filtered, the a * x product in f32 when the samples were f32
+    int mix_on, mix_a_f32;
+    double mix_a, mix_c;
 };
 
 template <int NS, bool R32, bool P2>
@@ -175,7 +193,14 @@ __device__ __forceinline__ void iir_op_pass(const IirOpArgs &a, int64_t g, int c
                 y = df2t(y, z[s][0], z[s][1], a.sos[s]);
                 if (R32) y = (double)(float)y;
             }
-            if (P2) a.out[((int64_t)pn * G + g) * CH + c] = y;
+            if (P2) {
+                if (a.mix_on) {  // numpy: samples + filtered * c, or samples * a + filtered * c
+                    const double ax = a.mix_a == 1.0 ? x
+                                      : (a.mix_a_f32 ? (double)__fmul_rn((float)x, (float)a.mix_a) : __dmul_rn(x, a.mix_a));
+                    y = __dadd_rn(ax, __dmul_rn(y, a.mix_c));
+                }
+                a.out[((int64_t)pn * G + g) * CH + c] = y;
+            }
             ++pn;
         });
 }
@@ -241,6 +266,35 @@ __global__ void __launch_bounds__(256) tile_energy_kernel(KwArgs a, const double
     a.part[2 * g] = e0;
     a.part[2 * g + 1] = e1;
     a.part_seg[g] = lo;
+}
+
+// Three natural int16 band arrays [N][CH] -> the compressor's tile-major band
+// planes (int16 pairs, mono R = 0) and per-tile energies E / tail, as the
+// crossover kernel leaves them (legacy engine: its bands come from other filters).
+template <int CH>
+__global__ void __launch_bounds__(256) bands_to_tiles_kernel(const int16_t *lo, const int16_t *mid, const int16_t *hi,
+                                                             short2 *plane0, short2 *plane1, short2 *plane2,
+                                                             double *tile_e, int64_t N, int64_t G, int Tl,
+                                                             int tf0, int tf1, int tf2) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int b = blockIdx.y;
+    if (g >= G) return;
+    const int16_t *in = b == 0 ? lo : (b == 1 ? mid : hi);
+    short2 *plane = b == 0 ? plane0 : (b == 1 ? plane1 : plane2);
+    const int tail_from = b == 0 ? tf0 : (b == 1 ? tf1 : tf2);
+    const int len = (int)min((int64_t)Tl, N - g * Tl);
+    double E = 0.0, tl = 0.0;
+    for (int n = 0; n < len; ++n) {
+        const int64_t f = g * Tl + n;
+        const int16_t x = in[f * CH];
+        const int16_t y = CH == 2 ? in[f * CH + 1] : (int16_t)0;
+        plane[(int64_t)n * G + g] = make_short2(x, y);
+        const double e = (double)((uint32_t)((int32_t)x * x) + (uint32_t)((int32_t)y * y));
+        E += e;
+        tl += n >= tail_from ? e : 0.0;
+    }
+    tile_e[(size_t)(2 * b) * G + g] = E;
+    tile_e[(size_t)(2 * b + 1) * G + g] = tl;
 }
 
 }  // namespace mm
@@ -319,7 +373,8 @@ int launch_iir_op(mm_ctx *c, int nsec, bool r32, unsigned nblk, const IirOpArgs 
 }
 
 // cascade f over a tile-major array in place (zero initial state, one line per channel)
-int iir_in_place(mm_ctx *c, const mm_iir *f, int64_t N, int ch, int64_t G, double *tm, int round_f32) {
+int iir_in_place(mm_ctx *c, const mm_iir *f, int64_t N, int ch, int64_t G, double *tm, int round_f32,
+                 const double *mix = nullptr, int mix_a_f32 = 0) {
     if (f->nsec < 1 || f->nsec > 4) return set_err(c, MM_ERR_ARG, "nsec %d out of [1, 4]", f->nsec);
     if (f->nsec_branch0 != f->nsec) return set_err(c, MM_ERR_ARG, "the operator filters ONE cascade");
     if (f->tpb != LB_THREADS / ch)
@@ -332,6 +387,12 @@ int iir_in_place(mm_ctx *c, const mm_iir *f, int64_t N, int ch, int64_t G, doubl
         for (int k = 0; k < 5; ++k) ia.sos[s][k] = s < f->nsec ? f->sos[s][k] : 0.0;
     ia.in = tm;
     ia.out = tm;
+    if (mix) {
+        ia.mix_on = 1;
+        ia.mix_a = mix[0];
+        ia.mix_c = mix[1];
+        ia.mix_a_f32 = mix_a_f32;
+    }
     LbArgs lb{};
     RET(upload_tables(c, "op_iir", *f, lb));
     const unsigned nblk = blocks_for(G, LB_THREADS / ch);
@@ -415,8 +476,30 @@ int mm_op_gain(mm_ctx *c, int dtype, const void *in, int64_t n, double gain, dou
     return PW_DISPATCH(PW_GAIN, dtype, in, (size_t)n * dtype_size(dtype), out, (size_t)n * 8, pa);
 }
 
-int mm_op_sosfilt(mm_ctx *c, int dtype, const void *in, int64_t frames, int channels, const mm_iir *f,
-                  int round_f32, double *out) {
+int mm_op_saturation_legacy(mm_ctx *c, int dtype, const void *in, int64_t n, double amount, void *out) {
+    if (!c || n < 0 || (n > 0 && (!in || !out))) return set_err(c, MM_ERR_ARG, "bad arguments");
+    RET(check_dtype(c, dtype));
+    HIPCHK(c, hipSetDevice(c->device));
+    PwArgs pa{};
+    pa.n = n;
+    pa.p0 = 1.0 + (amount / 100.0) * 4.0;  // main.py:95 (Python float)
+    const size_t bytes = (size_t)n * dtype_size(dtype);
+    return PW_DISPATCH(PW_SAT_LEGACY, dtype, in, bytes, out, bytes, pa);
+}
+
+int mm_op_soft_limiter_legacy(mm_ctx *c, int dtype, void *inout, int64_t n, double threshold) {
+    if (!c || n < 0 || (n > 0 && !inout)) return set_err(c, MM_ERR_ARG, "bad arguments");
+    RET(check_dtype(c, dtype));
+    HIPCHK(c, hipSetDevice(c->device));
+    PwArgs pa{};
+    pa.n = n;
+    pa.p0 = threshold;
+    const size_t bytes = (size_t)n * dtype_size(dtype);
+    return PW_DISPATCH(PW_LIMIT_LEGACY, dtype, inout, bytes, inout, bytes, pa);
+}
+
+static int sosfilt_common(mm_ctx *c, int dtype, const void *in, int64_t frames, int channels, const mm_iir *f,
+                          int round_f32, const double *mix, double *out) {
     if (!c || !f || frames < 0 || (frames > 0 && (!in || !out))) return set_err(c, MM_ERR_ARG, "bad arguments");
     if (channels != 1 && channels != 2) return set_err(c, MM_ERR_ARG, "channels must be 1 or 2");
     if (frames >= (int64_t)1 << 31) return set_err(c, MM_ERR_ARG, "more than 2^31 frames");
@@ -426,7 +509,7 @@ int mm_op_sosfilt(mm_ctx *c, int dtype, const void *in, int64_t frames, int chan
     const int64_t G = (frames + OPS_TILE - 1) / OPS_TILE;
     double *tm;
     RET(upload_tile_major(c, dtype, in, frames, channels, G, &tm));
-    RET(iir_in_place(c, f, frames, channels, G, tm, round_f32));
+    RET(iir_in_place(c, f, frames, channels, G, tm, round_f32, mix, dtype == MM_F32));
     double *dout;
     RET(get_buf(c, "op_out", (size_t)frames * channels, &dout));
     const unsigned nb = blocks_for(G, OPS_TILES);
@@ -441,6 +524,76 @@ int mm_op_sosfilt(mm_ctx *c, int dtype, const void *in, int64_t frames, int chan
     HIPCHK(c, hipStreamSynchronize(c->stream));
     resolve_events(c);
     return MM_OK;
+}
+
+int mm_op_sosfilt_mix(mm_ctx *c, int dtype, const void *in, int64_t frames, int channels, const mm_iir *f, double a,
+                      double cf, double *out) {
+    const double mix[2] = {a, cf};
+    return sosfilt_common(c, dtype, in, frames, channels, f, 0, mix, out);
+}
+
+// apply_multiband_compressor's compressor + overlay on three given int16 band
+// arrays [frames][channels] (the legacy engine's bands, main.py:156-177): the
+// chain's stage C on one line (job as for mm_op_multiband; its crossover unused).
+int mm_op_compress_bands(mm_ctx *c, const mm_job *j, const int16_t *lo, const int16_t *mid, const int16_t *hi,
+                         int16_t *out) {
+    if (!c || !j || (j->frames_proc > 0 && (!lo || !mid || !hi || !out))) return set_err(c, MM_ERR_ARG, "bad arguments");
+    if (!j->multiband_on || j->eq.nsec || j->sat_on || j->width_on || j->lufs_on)
+        return set_err(c, MM_ERR_ARG, "band compressor job: only the multiband stage may be on");
+    if (j->frames_in != j->frames_proc || (int64_t)j->tile * j->tiles_per_chunk < j->frames_proc)
+        return set_err(c, MM_ERR_ARG, "the operator's chunk must cover the whole input");
+    RET(validate(c, j));
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t N = j->frames_proc;
+    if (N == 0) return MM_OK;
+    const int T = j->tile, ch = j->channels;
+    const int64_t G = (N + T - 1) / T;
+    const int64_t TG = (int64_t)T * G;
+    c->G = G;
+    c->job = *j;
+    c->staged = false;
+    RET(setup_control(c, blocks_for(G, LB_THREADS / ch)));
+    const size_t bytes = (size_t)N * ch * 2;
+    char *din;
+    RET(get_buf(c, "host_in", 3 * bytes, &din));
+    HIPCHK(c, hipMemcpyAsync(din, lo, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(din + bytes, mid, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(din + 2 * bytes, hi, bytes, hipMemcpyHostToDevice, c->stream));
+    short2 *bands[3];
+    RET(get_buf(c, "band0", TG, &bands[0]));
+    RET(get_buf(c, "band1", TG, &bands[1]));
+    RET(get_buf(c, "band2", TG, &bands[2]));
+    double *tile_e;
+    RET(get_buf(c, "comp_tile_e", (size_t)6 * G, &tile_e));
+    int tf[3];
+    for (int b = 0; b < 3; ++b) {
+        const int r = j->band[b].look % T;
+        tf[b] = r ? T - r : T;
+    }
+    const int16_t *p0 = reinterpret_cast<const int16_t *>(din), *p1 = p0 + (size_t)N * ch, *p2 = p1 + (size_t)N * ch;
+    if (ch == 2)
+        RET(launch(c, "bands_to_tiles", bands_to_tiles_kernel<2>, dim3(blocks_for(G, 256), 3), dim3(256), 0, p0, p1, p2,
+                   bands[0], bands[1], bands[2], tile_e, N, G, T, tf[0], tf[1], tf[2]));
+    else
+        RET(launch(c, "bands_to_tiles", bands_to_tiles_kernel<1>, dim3(blocks_for(G, 256), 3), dim3(256), 0, p0, p1, p2,
+                   bands[0], bands[1], bands[2], tile_e, N, G, T, tf[0], tf[1], tf[2]));
+    short2 *q2;
+    RET(stage_compress(c, j, bands, tile_e, &q2));
+    c->mix = q2;
+    c->staged = true;
+    for (;;) {
+        bool converged;
+        RET(chain_check(c, &converged));
+        if (converged) break;
+        RET(comp_sweeps(c, 8));
+        RET(comp_back(c));
+    }
+    return mm_read_mix(c, out);
+}
+
+int mm_op_sosfilt(mm_ctx *c, int dtype, const void *in, int64_t frames, int channels, const mm_iir *f,
+                  int round_f32, double *out) {
+    return sosfilt_common(c, dtype, in, frames, channels, f, round_f32, nullptr, out);
 }
 
 // pyloudnorm Meter(rate).integrated_loudness of samples.mean(axis=1) (AME:213-218):

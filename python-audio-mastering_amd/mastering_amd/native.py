@@ -69,7 +69,8 @@ EXPORTS = ("mm_create", "mm_destroy", "mm_last_error", "mm_sync", "mm_version", 
            "mm_read_mix", "mm_timing", "mm_kernel_stats", "mm_comm_unique_id", "mm_comm_init", "mm_comm_destroy",
            "mm_allreduce_sum_f64", "mm_allgather_f64", "mm_wav_probe", "mm_master_wav",
            "mm_op_pcm_to_float", "mm_op_saturation", "mm_op_stereo_width", "mm_op_quantize", "mm_op_soft_limiter",
-           "mm_op_gain", "mm_op_sosfilt", "mm_op_loudness", "mm_op_multiband", "mm_master_batch")
+           "mm_op_gain", "mm_op_sosfilt", "mm_op_loudness", "mm_op_multiband", "mm_master_batch",
+           "mm_op_saturation_legacy", "mm_op_soft_limiter_legacy", "mm_op_sosfilt_mix", "mm_op_compress_bands")
 
 _lib = None
 _lock = threading.Lock()
@@ -125,6 +126,11 @@ def load():
                               ctypes.c_int),
             "mm_op_loudness": ([vp, P(MMJob), ctypes.c_int, vp, c_double_p], ctypes.c_int),
             "mm_op_multiband": ([vp, P(MMJob), vp, vp], ctypes.c_int),
+            "mm_op_saturation_legacy": ([vp, ctypes.c_int, vp, ctypes.c_int64, ctypes.c_double, vp], ctypes.c_int),
+            "mm_op_soft_limiter_legacy": ([vp, ctypes.c_int, vp, ctypes.c_int64, ctypes.c_double], ctypes.c_int),
+            "mm_op_sosfilt_mix": ([vp, ctypes.c_int, vp, ctypes.c_int64, ctypes.c_int, P(MMIir), ctypes.c_double,
+                                   ctypes.c_double, vp], ctypes.c_int),
+            "mm_op_compress_bands": ([vp, P(MMJob), vp, vp, vp, vp], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             fn = getattr(lib, name)
