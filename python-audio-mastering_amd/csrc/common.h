@@ -146,8 +146,9 @@ struct CompArgs {
     int64_t ocols;             // ceil(GS / own): pass-0 lanes per band
     int64_t RS;                // row stride of Mc / ck (own * ocols >= GS columns)
     double *start[3];          // per-super-tile start state
-    const double *end_in[3];
-    double *end_out[3];
+    double *end[3];            // per-super-tile end state (one buffer; sweeps hand ends over with sc1 accesses)
+    uint32_t *claim[3];        // per super-tile: the last sweep stamp that claimed it (zeroed per chain)
+    uint32_t stamp;            // this sweep's stamp (> every earlier one of the chain)
     unsigned int *changed;
     unsigned long long *walked;  // frames re-walked by the fix-up sweeps (statistics)
     short2 *q_out;

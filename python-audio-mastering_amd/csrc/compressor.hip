@@ -37,6 +37,7 @@
 // Sparse bands (the high band is active on ~0.1 % of pink-noise frames) thus
 // cost a few super-tiles per chunk, and dense ones ~frames/U.
 #include "common.h"
+#include "lookback.h"  // sc1 loads/stores and the global address-space types
 
 namespace mm {
 
@@ -283,7 +284,7 @@ __device__ __forceinline__ double lean_step(double att, double m, double inc, do
 // With CK (an owning walk), store the state on entry to every CK_Q-th frame.
 constexpr int WALK_WB = 32;  // M values in flight per walker
 constexpr int WALK_PAD = WALK_WB;  // padding rows after the compacted array (prefetch past a super-tile's end)
-constexpr int CK_Q = 8;      // checkpoint stride (compacted frames); divides WALK_WB, FIX_CHUNK and U
+constexpr int CK_Q = 8;      // checkpoint stride (compacted frames); divides WALK_WB and U
 
 template <bool CK>
 __device__ __forceinline__ double comp_walk(double att, const CompArgs &a, int b, int64_t s, int len,
@@ -341,22 +342,80 @@ __device__ __forceinline__ double comp_walk(double att, const CompArgs &a, int b
     return att;
 }
 
-// Compact streamed owning walk (checkpoints) for the fix kernel's lane path,
-// where the register budget is shared with the LDS-staged path.
-__device__ __forceinline__ double comp_walk_lean(double att, const CompArgs &a, int b, int64_t s, int len,
-                                                 const BandStep &bs) {
+// Re-walk of a super-tile by a fix sweep: comp_walk<true> from the corrected
+// start, which also compares the state at every WB-frame block start with the
+// checkpoint stored there by the previous walk (loaded one block ahead, before
+// this walk overwrites it).  Equal states mean the stored trajectory from there
+// on (and the stored end) came from the same state: the walk stops (coalesced).
+// Returns the end state (meaningless when coalesced); *nw = frames walked.
+__device__ __forceinline__ double comp_rewalk(double att, const CompArgs &a, int b, int64_t s, int len,
+                                              const BandStep &bs, bool *coalesced, int *nw) {
+    constexpr int WB = WALK_WB, WP = 4, CKB = WB / CK_Q;  // checkpoint rows per block
+    *coalesced = false;
+    *nw = len;
+    if (len <= 0) return att;
+    const size_t GS = (size_t)a.RS;
     const int64_t cs = cm_col(a, s);
-    const double *col = a.Mc[b] + cs;
-    double *ck = a.ck[b] + cs;
-    const uint32_t GS = (uint32_t)a.RS;
+    const double *pl = a.Mc[b] + cs;
+    double *pc = a.ck[b] + cs;
+    const double *po = pc;  // old checkpoint of the next block start (rows CKB apart; CKB padding rows)
+    double buf[WB], inc[WP], dec[WP];
+#pragma unroll
+    for (int k = 0; k < WB; ++k) {
+        buf[k] = *pl;
+        pl += GS;
+    }
+#pragma unroll
+    for (int k = 0; k < WP; ++k) {
+        inc[k] = div_cr(buf[k], bs.A, bs.rA);
+        dec[k] = div_cr(buf[k], bs.R, bs.rR);
+    }
+    double old = *po;
+    po += CKB * GS;
     int i = 0;
-    stream<8, 4, double>(
-        len, [&](int k) { return col[(uint32_t)min(k, len - 1) * GS]; },
-        [&](double m) {
-            if (i % CK_Q == 0) ck[(uint32_t)(i / CK_Q) * GS] = att;
-            att = comp_step(att, m, bs);
-            ++i;
-        });
+    for (; i + WB <= len; i += WB) {
+        if (__double_as_longlong(old) == __double_as_longlong(att)) {
+            *coalesced = true;
+            *nw = i;
+            return att;
+        }
+        old = *po;
+        po += CKB * GS;
+#pragma unroll
+        for (int k = 0; k < WB; ++k) {
+            const double m = buf[k], ik = inc[k % WP], dk = dec[k % WP];
+            const double mn = buf[(k + WP) % WB];
+            inc[k % WP] = div_cr(mn, bs.A, bs.rA);
+            dec[k % WP] = div_cr(mn, bs.R, bs.rR);
+            if (k % CK_Q == 0) {
+                *pc = att;
+                pc += GS;
+            }
+            att = lean_step(att, m, ik, dk);
+            buf[k] = *pl;
+            pl += GS;
+        }
+    }
+    const int rem = len - i;
+    if (rem > 0 && __double_as_longlong(old) == __double_as_longlong(att)) {
+        *coalesced = true;
+        *nw = i;
+        return att;
+    }
+#pragma unroll
+    for (int k = 0; k < WB; ++k) {
+        if (k < rem) {
+            const double m = buf[k], ik = inc[k % WP], dk = dec[k % WP];
+            const double mn = buf[(k + WP) % WB];
+            inc[k % WP] = div_cr(mn, bs.A, bs.rA);
+            dec[k % WP] = div_cr(mn, bs.R, bs.rR);
+            if (k % CK_Q == 0) {
+                *pc = att;
+                pc += GS;
+            }
+            att = lean_step(att, m, ik, dk);
+        }
+    }
     return att;
 }
 
@@ -398,105 +457,67 @@ __global__ void __launch_bounds__(PASS0_BLOCK) comp_pass0_kernel(CompArgs a) {
         }
         a.start[b][s] = att;
         att = comp_walk<true>(att, a, b, s, st.len, bs);
-        a.end_out[b][s] = att;
+        a.end[b][s] = att;
         warm = true;
     }
 }
 
-// 5. one Jacobi sweep (exits at once if the previous sweep changed nothing).
-// grid: (ceil(GS/64), 3), one wave per block, lane = super-tile.  A lane whose
-// start changed re-walks its super-tile.  When at most FIX_SLOTS lanes of the
-// wave walk (every sweep once the warm-up guesses are good), the wave serves
-// them together: chunk by chunk, all 64 lanes load the walkers' next M values
-// (prefetched one chunk ahead) and compute M/A and M/R into LDS, then every
-// walker runs the lean step (add, min, select: ~50 cycles instead of ~130 for a
-// lone lane that also divides; tools/micro/step_bench.hip) from LDS.
-constexpr int FIX_SLOTS = 16;   // walkers per wave served from LDS
-constexpr int FIX_CHUNK = 64;   // frames per walker per staging round
-constexpr int FIX_MAX_U = 8192; // cap on frames per super-tile (slot lengths are int)
+// 5. one fix-up sweep (exits at once if the previous sweep left nothing stale).
+// grid: (ceil(GS/64), 3), lane = super-tile.  A lane whose start differs from
+// its predecessor's end CLAIMS its super-tile (atomic max of the sweep stamp:
+// one writer per super-tile per sweep) and re-walks it from that end
+// (comp_rewalk: storing checkpoints, stopping once it meets the stored
+// trajectory, after which the stored trajectory and end are right).  A re-walk
+// that reaches the end without meeting it publishes the new end and CONTINUES
+// into the successor in the same chunk (whose stored trajectory started from
+// the old end) if it can claim it; if the successor's own lane claimed it
+// first, that lane may have read the old end, so the sweep flags `changed` and
+// the next sweep re-checks.  Every stale start is caught that way (a lane that
+// read an old end either lost the successor's claim to the continuing walker,
+// or the continuing walker lost it and flagged), so a sweep that flags nothing
+// leaves every start equal to its predecessor's end: exact by induction from
+// the chunk start.  Non-coalescing stretches (heavily compressed material) are
+// walked through in one sweep instead of one super-tile per sweep.
+constexpr int FIX_MAX_U = 8192; // cap on frames per super-tile (lengths are int)
+
+__device__ __forceinline__ bool comp_claim(const CompArgs &a, int b, int64_t s) {
+    return __hip_atomic_fetch_max((gu32 *)(a.claim[b] + s), a.stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+           a.stamp;
+}
 
 __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned int *prev_changed) {
-    __shared__ double sm[FIX_SLOTS][FIX_CHUNK + 1], si[FIX_SLOTS][FIX_CHUNK + 1], sd[FIX_SLOTS][FIX_CHUNK + 1];
-    __shared__ int slot_lane[FIX_SLOTS], slot_len[FIX_SLOTS];
-    __shared__ int64_t slot_col[FIX_SLOTS];
     if (prev_changed && *prev_changed == 0u) return;
-    const int lane = threadIdx.x;
-    const int64_t s = (int64_t)blockIdx.x * 64 + lane;
+    const int64_t s = (int64_t)blockIdx.x * 64 + threadIdx.x;
     const int b = blockIdx.y;
-    const bool valid = s < a.GS;
-    const Super st = valid ? super_of(a, b, s) : Super{0, 0, 0, false};
-    const bool live = valid && st.len > 0;
-    const double *end_in = a.end_in[b];
-    double e = live ? end_in[s] : 0.0;
-    double want = 0.0;
-    bool need = false;
-    if (live && st.p0 > 0) {
-        want = end_in[s - 1];
-        need = __double_as_longlong(want) != __double_as_longlong(a.start[b][s]);
-    }
+    if (s >= a.GS) return;
+    Super st = super_of(a, b, s);
+    if (st.len <= 0 || st.p0 == 0) return;  // chunk starts are exact
+    double *end = a.end[b];
+    double att = ld_sc1(end + s - 1);
+    if (__double_as_longlong(att) == __double_as_longlong(a.start[b][s])) return;
+    if (!comp_claim(a, b, s)) return;  // a walker continuing from s - 1 owns it
     const BandStep bs = band_step(a, b);
-    const unsigned long long m = __ballot(need);
-    const int k = __popcll(m);
-    if (k > FIX_SLOTS) {
-        if (need) e = comp_walk_lean(want, a, b, s, st.len, bs);
-    } else if (k > 0) {
-        const int slot = __popcll(m & ((1ull << lane) - 1));
-        if (need) {
-            slot_lane[slot] = lane;
-            slot_len[slot] = st.len;
-            slot_col[slot] = cm_col(a, s);
+    unsigned long long walked = 0;
+    int64_t cur = s;
+    for (;;) {
+        a.start[b][cur] = att;
+        bool coalesced;
+        int nw;
+        const double t = comp_rewalk(att, a, b, cur, st.len, bs, &coalesced, &nw);
+        walked += nw;
+        if (coalesced) break;
+        st_sc1(end + cur, t);
+        if (st.last) break;  // the chunk's last super-tile: no successor
+        const int64_t nxt = cur + 1;
+        if (!comp_claim(a, b, nxt)) {
+            *a.changed = 1u;  // benign race: every writer stores 1
+            break;
         }
-        __syncthreads();
-        int maxlen = 0;
-        for (int w = 0; w < k; ++w) maxlen = max(maxlen, slot_len[w]);
-        const double *Mc = a.Mc[b];
-        const int64_t col0 = (int64_t)blockIdx.x * 64;
-        double pre[FIX_SLOTS];  // lane = frame offset in the chunk, r = walker slot
-        auto load_chunk = [&](int base) {
-#pragma unroll
-            for (int r = 0; r < FIX_SLOTS; ++r) {
-                if (r < k) {
-                    const int i = base + lane;
-                    pre[r] = i < slot_len[r] ? Mc[(int64_t)i * a.RS + slot_col[r]] : 0.0;
-                }
-            }
-        };
-        load_chunk(0);
-        double att = want;
-        for (int base = 0; base < maxlen; base += FIX_CHUNK) {
-#pragma unroll
-            for (int r = 0; r < FIX_SLOTS; ++r) {
-                if (r < k) {
-                    const double mv = pre[r];
-                    sm[r][lane] = mv;
-                    si[r][lane] = div_cr(mv, bs.A, bs.rA);
-                    sd[r][lane] = div_cr(mv, bs.R, bs.rR);
-                }
-            }
-            __syncthreads();
-            if (base + FIX_CHUNK < maxlen) load_chunk(base + FIX_CHUNK);
-            if (need) {
-                const int lim = min(FIX_CHUNK, st.len - base);
-                const double *pm = sm[slot], *pi = si[slot], *pd = sd[slot];
-                double *ck = a.ck[b] + slot_col[slot] + (int64_t)(base / CK_Q) * a.RS;
-#pragma unroll 8
-                for (int f = 0; f < lim; ++f) {
-                    if (f % CK_Q == 0) ck[(int64_t)(f / CK_Q) * a.RS] = att;  // base is a multiple of CK_Q
-                    const double up = fmin(att + pi[f], pm[f]);
-                    const double dn = fmax(att - pd[f], 0.0);
-                    att = att <= pm[f] ? up : dn;
-                }
-            }
-            __syncthreads();
-        }
-        if (need) e = att;
+        att = t;
+        cur = nxt;
+        st = super_of(a, b, cur);
     }
-    if (need) {
-        a.start[b][s] = want;
-        *a.changed = 1u;  // benign race: every writer stores 1
-        atomicAdd(a.walked, (unsigned long long)st.len);
-    }
-    if (live) a.end_out[b][s] = e;
+    atomicAdd(a.walked, walked);
 }
 
 // compacted index p of chunk c -> element address in the super-tile-major array
@@ -521,9 +542,16 @@ __device__ __forceinline__ double comp_state_at(const CompArgs &a, int b, int64_
 }
 
 // 7. gains + overlay.  A block = 64 tiles x 3 bands: wave w runs band w's exact
-// trajectory from tstart for its 64 tiles (audioop.mul floor on both channels),
-// 8 frames at a time into LDS; then all 192 threads overlay
+// trajectory for its 64 tiles from the checkpoints (audioop.mul floor on both
+// channels), APPLY_STEP frames at a time into LDS; then all 192 threads overlay
 // sat16(sat16(lo + mid) + hi) (AME:210) and store q2 coalesced.
+// Branch-free per frame so a group's steps, gains and multiplies interleave:
+//  * M == 0 (rms <= threshold) needs no test: the step is then the identity;
+//  * att == 0 gives gain 10^-0 = 1.0 exactly, for which audioop.mul is the
+//    identity (pydub skips the multiply there);
+//  * the group's 10^(-att/20) are skipped (wave-uniformly) when no lane's att
+//    changed since the last gain (the sparse band's wave, almost always).
+// Loads run two groups ahead (R, samples) and the table gathers one group ahead.
 #ifndef MM_APPLY_STEP
 #define MM_APPLY_STEP 8
 #endif
@@ -538,7 +566,8 @@ __device__ __forceinline__ double neg_div20(double att) {
 }
 
 __global__ void __launch_bounds__(192) comp_apply_kernel(CompArgs a) {
-    __shared__ short2 lds[3][APPLY_STEP][APPLY_TILES];
+    constexpr int S = APPLY_STEP;
+    __shared__ short2 lds[3][S][APPLY_TILES];
     const int b = threadIdx.x / APPLY_TILES;
     const int lane = threadIdx.x % APPLY_TILES;
     const int64_t G = a.G;
@@ -552,48 +581,69 @@ __global__ void __launch_bounds__(192) comp_apply_kernel(CompArgs a) {
     const uint16_t *R = a.r16[b];
     const short2 *X = a.band[b];
     double att = valid ? comp_state_at(a, b, g / a.K, a.off[b][g], bs) : 0.0;
-    double gain = 1.0, gain_att = -1.0;  // gain = db_to_float(-gain_att); att >= 0 never equals -1
-    uint16_t rn[APPLY_STEP];
-    short2 vn[APPLY_STEP];
-    auto prefetch = [&](int n0) {
+    double gain = 1.0, gain_att = -1.0;  // gain of gain_att; att >= 0 never equals -1
+    const uint32_t G32 = (uint32_t)G, gl = valid ? (uint32_t)g : 0u;
+    const int last = max(len - 1, 0);
+    uint16_t r1[S], r2[S];
+    short2 v1[S], v2[S];
+    double m1[S];
+    auto load = [&](int n0, uint16_t (&r)[S], short2 (&v)[S]) {
 #pragma unroll
-        for (int j = 0; j < APPLY_STEP; ++j) {
-            const int n = min(n0 + j, max(len - 1, 0));
-            const int64_t idx = (int64_t)n * G + (valid ? g : 0);
-            rn[j] = R[idx];
-            vn[j] = X[idx];
+        for (int j = 0; j < S; ++j) {
+            const uint32_t idx = (uint32_t)min(n0 + j, last) * G32 + gl;
+            r[j] = R[idx];
+            v[j] = X[idx];
         }
     };
-    prefetch(0);
-    for (int n0 = 0; n0 < T; n0 += APPLY_STEP) {
-        short2 v[APPLY_STEP];
-        double m[APPLY_STEP];
+    // frames past the tile's end read lut[0] = 0 (rms 0 is below every threshold:
+    // the identity step; their output is unused).  The index select keeps the
+    // gather unconditional (a conditional load would be an exec-mask branch).
+    auto gather = [&](int n0, const uint16_t (&r)[S], double (&m)[S]) {
 #pragma unroll
-        for (int j = 0; j < APPLY_STEP; ++j) {
-            v[j] = vn[j];
-            m[j] = lut[rn[j]];
+        for (int j = 0; j < S; ++j) m[j] = lut[n0 + j < len ? r[j] : 0];
+    };
+    load(0, r1, v1);
+    load(S, r2, v2);
+    gather(0, r1, m1);
+    for (int n0 = 0; n0 < T; n0 += S) {
+        // this group: v1, m1; next: r2, v2
+        short2 v[S];
+        double m[S];
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+            v[j] = v1[j];
+            m[j] = m1[j];
+            v1[j] = v2[j];
         }
-        if (n0 + APPLY_STEP < T) prefetch(n0 + APPLY_STEP);
+        gather(n0 + S, r2, m1);
+        load(n0 + 2 * S, r2, v2);
+        double at[S];
+        bool same = true;
 #pragma unroll
-        for (int j = 0; j < APPLY_STEP; ++j) {
-            if (n0 + j < len) {
-                // M == 0 (rms <= threshold) is the identity step, and the gain only
-                // changes with att: the sparse band's wave skips both almost always
-                if (m[j] != 0.0) att = comp_step(att, m[j], bs);
-                short2 s = v[j];
-                if (att != 0.0) {
-                    if (att != gain_att) {
-                        gain = exp10(neg_div20(att));  // db_to_float(-att)
-                        gain_att = att;
-                    }
-                    s.x = audioop_mul(s.x, gain);
-                    s.y = audioop_mul(s.y, gain);
-                }
-                lds[b][j][lane] = s;
-            }
+        for (int j = 0; j < S; ++j) {
+            att = lean_step(att, m[j], div_cr(m[j], bs.A, bs.rA), div_cr(m[j], bs.R, bs.rR));
+            at[j] = att;
+            same = same && att == gain_att;
+        }
+        double gj[S];
+        if (__all(same)) {  // wave-uniform: no lane's attenuation moved
+#pragma unroll
+            for (int j = 0; j < S; ++j) gj[j] = gain;
+        } else {
+#pragma unroll
+            for (int j = 0; j < S; ++j) gj[j] = exp10(neg_div20(at[j]));  // db_to_float(-att); exp10(-0) == 1 exactly
+            gain = gj[S - 1];
+            gain_att = at[S - 1];
+        }
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+            short2 s = v[j];
+            s.x = audioop_mul(s.x, gj[j]);
+            s.y = audioop_mul(s.y, gj[j]);
+            lds[b][j][lane] = s;
         }
         lds_barrier();
-        for (int p = threadIdx.x; p < APPLY_STEP * APPLY_TILES; p += 3 * APPLY_TILES) {
+        for (int p = threadIdx.x; p < S * APPLY_TILES; p += 3 * APPLY_TILES) {
             const int j = p / APPLY_TILES, tl = p % APPLY_TILES;
             const int64_t gt = g0 + tl;
             const int n = n0 + j;

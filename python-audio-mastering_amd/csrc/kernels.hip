@@ -8,10 +8,11 @@ namespace mm {
 
 // audioop.mul of one int16 sample (pydub compressor output, AME:207-209).
 __device__ __forceinline__ int16_t audioop_mul(int16_t x, double g) {
-    double v = (double)x * g;
-    if (v > 32767.0) v = 32767.0;
-    else if (v < -32767.0) v = -32768.0;
-    return (int16_t)(int32_t)floor(v);
+    // audioop's "v > 32767 -> 32767; v < -32767 -> -32768; floor(v)" equals
+    // floor(v) clamped to [-32768, 32767] (v in (-32768, -32767) floors to
+    // -32768 too); min/max instead of branches
+    const double v = floor(__builtin_fmin(__builtin_fmax((double)x * g, -32768.0), 32767.0));
+    return (int16_t)(int32_t)v;
 }
 
 __device__ __forceinline__ int16_t sat16(int32_t v) {

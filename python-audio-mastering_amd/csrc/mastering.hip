@@ -58,7 +58,7 @@ struct mm_ctx {
     // compressor state kept across the queued launches (stage_front -> comp_sweeps/comp_back)
     bool comp_on = false;
     CompArgs ca{};
-    double *comp_cur = nullptr, *comp_nxt = nullptr;
+    uint32_t comp_stamp = 0;  // stamp of the last queued fix-up sweep
     unsigned *comp_changed = nullptr;
     int comp_iters = 0, comp_pending = 0;
     unsigned comp_nb = 0;
@@ -291,10 +291,10 @@ static int launch_eq(mm_ctx *c, int nsec, int ch, unsigned nblk, const EqArgs &e
 }
 
 // --------------------------------------------------- compressor sweeps
-// Jacobi sweeps are queued without a host sync: sweep k writes flag k and exits
-// at once if sweep k-1 changed nothing (so after the first quiet sweep both end
-// buffers hold the converged ends).  Convergence is checked at the chain's
-// single sync (comp_check); a rare unconverged batch is extended there.
+// Fix-up sweeps are queued without a host sync: sweep k writes flag k (some
+// successor may be stale) and exits at once if sweep k-1 flagged nothing.
+// Convergence is checked at the chain's single sync (evaluate_chain); a rare
+// unconverged batch is extended there (MM_COMP_SWEEPS sets the queued count).
 constexpr int COMP_SWEEPS = 6;  // queued per chain; more resume from the host (more sweeps, then apply again)
 
 static int comp_sweeps(mm_ctx *c, int n) {
@@ -304,14 +304,10 @@ static int comp_sweeps(mm_ctx *c, int n) {
         HIPCHK(c, hipMemsetAsync(c->comp_changed, 0, 16 * sizeof(unsigned int), c->stream));
     c->comp_flags_fresh = false;
     for (int k = 0; k < n; ++k) {
-        for (int b = 0; b < 3; ++b) {
-            ca.end_in[b] = c->comp_cur + (size_t)b * NS;
-            ca.end_out[b] = c->comp_nxt + (size_t)b * NS;
-        }
+        ca.stamp = ++c->comp_stamp;
         ca.changed = c->comp_changed + k;
         const unsigned int *prevf = k > 0 ? c->comp_changed + (k - 1) : nullptr;
         RET(launch(c, "comp_fix", comp_fix_kernel, dim3(blocks_for(NS, 64), 3), dim3(64), 0, ca, prevf));
-        std::swap(c->comp_cur, c->comp_nxt);
     }
     c->comp_pending = n;
     return MM_OK;
@@ -436,11 +432,13 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     ca.ocols = (NS + ca.own - 1) / ca.own;
     ca.RS = ca.ocols * ca.own;
     const int64_t RS = ca.RS;
-    double *st, *eA, *eB, *luts, *cks;
+    double *st, *ends, *luts, *cks;
+    uint32_t *claims;
     RET(get_buf(c, "comp_start", (size_t)3 * NS, &st));
-    RET(get_buf(c, "comp_endA", (size_t)3 * NS, &eA));
-    RET(get_buf(c, "comp_endB", (size_t)3 * NS, &eB));
-    RET(get_buf(c, "comp_ck", (size_t)3 * RS * (ca.U / CK_Q), &cks));
+    RET(get_buf(c, "comp_end", (size_t)3 * NS, &ends));
+    RET(get_buf(c, "comp_claim", (size_t)3 * NS, &claims));
+    HIPCHK(c, hipMemsetAsync(claims, 0, (size_t)3 * NS * sizeof(uint32_t), c->stream));
+    RET(get_buf(c, "comp_ck", (size_t)3 * RS * (ca.U / CK_Q + WALK_WB / CK_Q), &cks));  // + rows read ahead by re-walks
     RET(get_buf(c, "comp_lut", (size_t)3 * 32769, &luts));
     unsigned int *changed = c->comp_changed;  // zeroed with the chain's control words
     ca.walked = reinterpret_cast<unsigned long long *>(changed + 32);
@@ -480,8 +478,9 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
         ca.off[b] = off + (size_t)b * G;
         ca.total[b] = tot + (size_t)b * nchunks;
         ca.start[b] = st + (size_t)b * NS;
-        ca.ck[b] = cks + (size_t)b * RS * (ca.U / CK_Q);
-        ca.end_out[b] = eA + (size_t)b * NS;
+        ca.ck[b] = cks + (size_t)b * RS * (ca.U / CK_Q + WALK_WB / CK_Q);
+        ca.end[b] = ends + (size_t)b * NS;
+        ca.claim[b] = claims + (size_t)b * NS;
     }
     RET(launch(c, "comp_rms", comp_rms_kernel, dim3(nb, 3), dim3(256), 0, ca));
     RET(launch(c, "comp_offsets", comp_offsets_kernel, dim3((unsigned)nchunks, 3), dim3(1024), 0, ca));
@@ -490,13 +489,14 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
                dim3(blocks_for((NS + ca.own - 1) / ca.own, PASS0_BLOCK), 3), dim3(PASS0_BLOCK), 0, ca));
     c->comp_on = true;
     c->ca = ca;
-    c->comp_cur = eA;
-    c->comp_nxt = eB;
+    c->comp_stamp = 0;
     c->comp_changed = changed;
     c->comp_iters = 0;
     c->comp_pending = 0;
     c->comp_nb = nb;
-    RET(comp_sweeps(c, COMP_SWEEPS));
+    int sweeps = COMP_SWEEPS;
+    if (const char *e = getenv("MM_COMP_SWEEPS")) sweeps = std::max(1, std::min(64, atoi(e)));  // tests / tuning
+    RET(comp_sweeps(c, sweeps));
     RET(comp_back(c));
     return MM_OK;
 }
