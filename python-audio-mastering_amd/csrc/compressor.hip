@@ -582,6 +582,14 @@ __global__ void __launch_bounds__(192) comp_apply_kernel(CompArgs a) {
     const short2 *X = a.band[b];
     double att = valid ? comp_state_at(a, b, g / a.K, a.off[b][g], bs) : 0.0;
     double gain = 1.0, gain_att = -1.0;  // gain of gain_att; att >= 0 never equals -1
+    // a wave whose 64 tiles hold no active frame (the sparse band, almost
+    // everywhere) keeps each tile's entry state: one constant gain per lane, no
+    // rms loads, table gathers or steps
+    const bool quiet = __all(!valid || a.cnt[b][g] == 0);
+    if (quiet) {
+        gain = exp10(neg_div20(att));
+        gain_att = att;
+    }
     const uint32_t G32 = (uint32_t)G, gl = valid ? (uint32_t)g : 0u;
     const int last = max(len - 1, 0);
     uint16_t r1[S], r2[S];
@@ -615,25 +623,34 @@ __global__ void __launch_bounds__(192) comp_apply_kernel(CompArgs a) {
             m[j] = m1[j];
             v1[j] = v2[j];
         }
-        gather(n0 + S, r2, m1);
-        load(n0 + 2 * S, r2, v2);
-        double at[S];
-        bool same = true;
-#pragma unroll
-        for (int j = 0; j < S; ++j) {
-            att = lean_step(att, m[j], div_cr(m[j], bs.A, bs.rA), div_cr(m[j], bs.R, bs.rR));
-            at[j] = att;
-            same = same && att == gain_att;
-        }
         double gj[S];
-        if (__all(same)) {  // wave-uniform: no lane's attenuation moved
+        if (quiet) {  // wave-uniform: only the samples stream
 #pragma unroll
-            for (int j = 0; j < S; ++j) gj[j] = gain;
+            for (int j = 0; j < S; ++j) {
+                const uint32_t idx = (uint32_t)min(n0 + 2 * S + j, last) * G32 + gl;
+                v2[j] = X[idx];
+                gj[j] = gain;
+            }
         } else {
+            gather(n0 + S, r2, m1);
+            load(n0 + 2 * S, r2, v2);
+            double at[S];
+            bool same = true;
 #pragma unroll
-            for (int j = 0; j < S; ++j) gj[j] = exp10(neg_div20(at[j]));  // db_to_float(-att); exp10(-0) == 1 exactly
-            gain = gj[S - 1];
-            gain_att = at[S - 1];
+            for (int j = 0; j < S; ++j) {
+                att = lean_step(att, m[j], div_cr(m[j], bs.A, bs.rA), div_cr(m[j], bs.R, bs.rR));
+                at[j] = att;
+                same = same && att == gain_att;
+            }
+            if (__all(same)) {  // wave-uniform: no lane's attenuation moved
+#pragma unroll
+                for (int j = 0; j < S; ++j) gj[j] = gain;
+            } else {
+#pragma unroll
+                for (int j = 0; j < S; ++j) gj[j] = exp10(neg_div20(at[j]));  // db_to_float(-att); exp10(-0) == 1 exactly
+                gain = gj[S - 1];
+                gain_att = at[S - 1];
+            }
         }
 #pragma unroll
         for (int j = 0; j < S; ++j) {
