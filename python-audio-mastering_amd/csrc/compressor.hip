@@ -163,6 +163,11 @@ __device__ __forceinline__ int64_t cm_col(const CompArgs &a, int64_t s) {
     return (s % a.own) * a.ocols + s / a.own;
 }
 
+#ifndef MM_COMPACT_B
+#define MM_COMPACT_B 8
+#endif
+constexpr int COMPACT_B = MM_COMPACT_B;  // frames per gather block (the table gathers run one block ahead)
+
 // 3. scatter M of active frames into the compacted array.  grid (ceil(G/256), 3)
 // Inactive frames store into this lane's own padding slot (row U of the array),
 // so every store is unconditional; the element index is 32-bit and advanced
@@ -185,7 +190,7 @@ __global__ void __launch_bounds__(256) comp_compact_kernel(CompArgs a) {
     uint32_t idx = o * RS + col;  // its element
     const uint32_t dummy = U * RS + g32 % RS;
     double *Mc = a.Mc[b];
-    stream2<8, 2, uint16_t, double>(
+    stream2<COMPACT_B, 2, uint16_t, double>(
         len, [&](int i) { return R[(uint32_t)min(i, len - 1) * G32]; },
         [&](uint16_t r) { return lut[r]; },
         [&](uint16_t r, double m) {
