@@ -58,6 +58,10 @@ typedef struct mm_iir {
     int32_t nsec_branch0;    /* sections in branch 0 (rest are branch 1)      */
     int32_t dim;             /* state dim per channel = 2 * nsec              */
     int32_t tpb;             /* tiles per block the block powers were made for */
+    int32_t tile;            /* frames per tile the tile powers were made for (the
+                                job's tile; K-weighting: a divisor of it, its
+                                lanes then run tile/kweight.tile sub-tiles each) */
+    int32_t _pad;
     double sos[4][5];
     double phi_tile_pow[MM_TILE_POW][MM_MAX_DIM * MM_MAX_DIM];
     double phi_blk_pow[MM_BLK_POW][MM_MAX_DIM * MM_MAX_DIM];

@@ -145,6 +145,8 @@ struct CompArgs {
     int own;                   // super-tiles walked per pass-0 lane (after one warm-up)
     int64_t ocols;             // ceil(GS / own): pass-0 lanes per band
     int64_t RS;                // row stride of Mc / ck (own * ocols >= GS columns)
+    uint32_t mc_bytes, ck_bytes;  // bytes of one band's Mc / ck (buffer descriptors)
+    int buf_ok;                // both under 2 GB: walks use buffer loads (compressor.hip ColWalk)
     double *start[3];          // per-super-tile start state
     double *end[3];            // per-super-tile end state (one buffer; sweeps hand ends over with sc1 accesses)
     uint32_t *claim[3];        // per super-tile: the last sweep stamp that claimed it (zeroed per chain)

@@ -164,9 +164,15 @@ __device__ __forceinline__ int64_t cm_col(const CompArgs &a, int64_t s) {
 }
 
 #ifndef MM_COMPACT_B
-#define MM_COMPACT_B 8
+#define MM_COMPACT_B 32
 #endif
-constexpr int COMPACT_B = MM_COMPACT_B;  // frames per gather block (the table gathers run one block ahead)
+#ifndef MM_COMPACT_NB
+#define MM_COMPACT_NB 2
+#endif
+// frames per gather block (the table gathers run one block ahead; C2: 0.18 ms at 8,
+// 0.16 at 16, 0.15 at 32 (208 VGPRs: fewer waves, more gathers in flight)) and rms
+// blocks in flight
+constexpr int COMPACT_B = MM_COMPACT_B, COMPACT_NB = MM_COMPACT_NB;
 
 // 3. scatter M of active frames into the compacted array.  grid (ceil(G/256), 3)
 // Inactive frames store into this lane's own padding slot (row U of the array),
@@ -190,7 +196,7 @@ __global__ void __launch_bounds__(256) comp_compact_kernel(CompArgs a) {
     uint32_t idx = o * RS + col;  // its element
     const uint32_t dummy = U * RS + g32 % RS;
     double *Mc = a.Mc[b];
-    stream2<COMPACT_B, 2, uint16_t, double>(
+    stream2<COMPACT_B, COMPACT_NB, uint16_t, double>(
         len, [&](int i) { return R[(uint32_t)min(i, len - 1) * G32]; },
         [&](uint16_t r) { return lut[r]; },
         [&](uint16_t r, double m) {
@@ -291,22 +297,59 @@ constexpr int WALK_WB = 32;  // M values in flight per walker
 constexpr int WALK_PAD = WALK_WB;  // padding rows after the compacted array (prefetch past a super-tile's end)
 constexpr int CK_Q = 8;      // checkpoint stride (compacted frames); divides WALK_WB and U
 
-template <bool CK>
+// A column of Mc / ck walked row by row.  BUF: buffer loads/stores with the
+// column's byte offset in a VGPR (constant over the walk) and the row's in an
+// SGPR (the rows of a walk are wave-uniform), so stepping costs no VALU address
+// arithmetic; needs the array under 2 GB (CompArgs::buf_ok).  Else flat pointers.
+template <bool BUF>
+struct ColWalk;
+template <>
+struct ColWalk<false> {
+    double *p;
+    size_t step;
+    __device__ __forceinline__ ColWalk(const double *base, int64_t col, int64_t rs, uint32_t)
+        : p(const_cast<double *>(base) + col), step((size_t)rs) {}
+    __device__ __forceinline__ double ld() {
+        const double v = *p;
+        p += step;
+        return v;
+    }
+    __device__ __forceinline__ void st(double v) {
+        *p = v;
+        p += step;
+    }
+};
+template <>
+struct ColWalk<true> {
+    __amdgpu_buffer_rsrc_t r;
+    int vo, so, step;
+    __device__ __forceinline__ ColWalk(const double *base, int64_t col, int64_t rs, uint32_t bytes)
+        : r(__builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(base), (short)0, (int)bytes, 0x00020000)),
+          vo((int)(col * 8)), so(0), step((int)(rs * 8)) {}
+    __device__ __forceinline__ double ld() {
+        const double v = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0));
+        so += step;
+        return v;
+    }
+    __device__ __forceinline__ void st(double v) {
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, vo, so, 0);
+        so += step;
+    }
+};
+
+template <bool CK, bool BUF = false>
 __device__ __forceinline__ double comp_walk(double att, const CompArgs &a, int b, int64_t s, int len,
                                             const BandStep &bs) {
     constexpr int WB = WALK_WB, WP = 4;
     if (len <= 0) return att;
-    // column s, rows GS apart; loads run up to WB rows past the end (padding rows)
-    const size_t GS = (size_t)a.RS;  // row stride
+    // column s, rows RS apart; loads run up to WB rows past the end (padding rows)
     const int64_t cs = cm_col(a, s);
-    const double *pl = a.Mc[b] + cs;
-    double *pc = CK ? a.ck[b] + cs : nullptr;  // checkpoint rows, one row stride apart
+    ColWalk<BUF> pl(a.Mc[b], cs, a.RS, a.mc_bytes);
+    ColWalk<BUF> pc(CK ? a.ck[b] : a.Mc[b], cs, a.RS, a.ck_bytes);  // checkpoint rows
     double buf[WB], inc[WP], dec[WP];
 #pragma unroll
-    for (int k = 0; k < WB; ++k) {
-        buf[k] = *pl;
-        pl += GS;
-    }
+    for (int k = 0; k < WB; ++k) buf[k] = pl.ld();
 #pragma unroll
     for (int k = 0; k < WP; ++k) {
         inc[k] = div_cr(buf[k], bs.A, bs.rA);
@@ -320,13 +363,9 @@ __device__ __forceinline__ double comp_walk(double att, const CompArgs &a, int b
             const double mn = buf[(k + WP) % WB];  // frame i+k+WP (already reloaded when k+WP >= WB)
             inc[k % WP] = div_cr(mn, bs.A, bs.rA);
             dec[k % WP] = div_cr(mn, bs.R, bs.rR);
-            if (CK && k % CK_Q == 0) {
-                *pc = att;
-                pc += GS;
-            }
+            if (CK && k % CK_Q == 0) pc.st(att);
             att = lean_step(att, m, ik, dk);
-            buf[k] = *pl;
-            pl += GS;
+            buf[k] = pl.ld();
         }
     }
     const int rem = len - i;
@@ -337,10 +376,7 @@ __device__ __forceinline__ double comp_walk(double att, const CompArgs &a, int b
             const double mn = buf[(k + WP) % WB];
             inc[k % WP] = div_cr(mn, bs.A, bs.rA);
             dec[k % WP] = div_cr(mn, bs.R, bs.rR);
-            if (CK && k % CK_Q == 0) {
-                *pc = att;
-                pc += GS;
-            }
+            if (CK && k % CK_Q == 0) pc.st(att);
             att = lean_step(att, m, ik, dk);
         }
     }
@@ -353,30 +389,26 @@ __device__ __forceinline__ double comp_walk(double att, const CompArgs &a, int b
 // this walk overwrites it).  Equal states mean the stored trajectory from there
 // on (and the stored end) came from the same state: the walk stops (coalesced).
 // Returns the end state (meaningless when coalesced); *nw = frames walked.
+template <bool BUF>
 __device__ __forceinline__ double comp_rewalk(double att, const CompArgs &a, int b, int64_t s, int len,
                                               const BandStep &bs, bool *coalesced, int *nw) {
     constexpr int WB = WALK_WB, WP = 4, CKB = WB / CK_Q;  // checkpoint rows per block
     *coalesced = false;
     *nw = len;
     if (len <= 0) return att;
-    const size_t GS = (size_t)a.RS;
     const int64_t cs = cm_col(a, s);
-    const double *pl = a.Mc[b] + cs;
-    double *pc = a.ck[b] + cs;
-    const double *po = pc;  // old checkpoint of the next block start (rows CKB apart; CKB padding rows)
+    ColWalk<BUF> pl(a.Mc[b], cs, a.RS, a.mc_bytes);
+    ColWalk<BUF> pc(a.ck[b], cs, a.RS, a.ck_bytes);
+    ColWalk<BUF> po(a.ck[b], cs, CKB * a.RS, a.ck_bytes);  // old checkpoint of the next block start (padding rows)
     double buf[WB], inc[WP], dec[WP];
 #pragma unroll
-    for (int k = 0; k < WB; ++k) {
-        buf[k] = *pl;
-        pl += GS;
-    }
+    for (int k = 0; k < WB; ++k) buf[k] = pl.ld();
 #pragma unroll
     for (int k = 0; k < WP; ++k) {
         inc[k] = div_cr(buf[k], bs.A, bs.rA);
         dec[k] = div_cr(buf[k], bs.R, bs.rR);
     }
-    double old = *po;
-    po += CKB * GS;
+    double old = po.ld();
     int i = 0;
     for (; i + WB <= len; i += WB) {
         if (__double_as_longlong(old) == __double_as_longlong(att)) {
@@ -384,21 +416,16 @@ __device__ __forceinline__ double comp_rewalk(double att, const CompArgs &a, int
             *nw = i;
             return att;
         }
-        old = *po;
-        po += CKB * GS;
+        old = po.ld();
 #pragma unroll
         for (int k = 0; k < WB; ++k) {
             const double m = buf[k], ik = inc[k % WP], dk = dec[k % WP];
             const double mn = buf[(k + WP) % WB];
             inc[k % WP] = div_cr(mn, bs.A, bs.rA);
             dec[k % WP] = div_cr(mn, bs.R, bs.rR);
-            if (k % CK_Q == 0) {
-                *pc = att;
-                pc += GS;
-            }
+            if (k % CK_Q == 0) pc.st(att);
             att = lean_step(att, m, ik, dk);
-            buf[k] = *pl;
-            pl += GS;
+            buf[k] = pl.ld();
         }
     }
     const int rem = len - i;
@@ -414,10 +441,7 @@ __device__ __forceinline__ double comp_rewalk(double att, const CompArgs &a, int
             const double mn = buf[(k + WP) % WB];
             inc[k % WP] = div_cr(mn, bs.A, bs.rA);
             dec[k % WP] = div_cr(mn, bs.R, bs.rR);
-            if (k % CK_Q == 0) {
-                *pc = att;
-                pc += GS;
-            }
+            if (k % CK_Q == 0) pc.st(att);
             att = lean_step(att, m, ik, dk);
         }
     }
@@ -437,6 +461,8 @@ __device__ __forceinline__ double comp_rewalk(double att, const CompArgs &a, int
 #endif
 constexpr int PASS0_BLOCK = MM_PASS0_BLOCK;
 
+// (flat column walks: the buffer-load form measured slower here, 0.27 -> 0.30 ms on
+// C2, though it helps the sweeps' lone walkers)
 __global__ void __launch_bounds__(PASS0_BLOCK) comp_pass0_kernel(CompArgs a) {
     const int64_t s0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * a.own;
     const int b = blockIdx.y;
@@ -490,6 +516,7 @@ __device__ __forceinline__ bool comp_claim(const CompArgs &a, int b, int64_t s) 
            a.stamp;
 }
 
+template <bool BUF>
 __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned int *prev_changed) {
     if (prev_changed && *prev_changed == 0u) return;
     const int64_t s = (int64_t)blockIdx.x * 64 + threadIdx.x;
@@ -508,7 +535,7 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
         a.start[b][cur] = att;
         bool coalesced;
         int nw;
-        const double t = comp_rewalk(att, a, b, cur, st.len, bs, &coalesced, &nw);
+        const double t = comp_rewalk<BUF>(att, a, b, cur, st.len, bs, &coalesced, &nw);
         walked += nw;
         if (coalesced) break;
         st_sc1(end + cur, t);
@@ -541,8 +568,15 @@ __device__ __forceinline__ double comp_state_at(const CompArgs &a, int b, int64_
     int32_t q = p - p % CK_Q;
     if (q >= L) q -= CK_Q;
     const int32_t k = q / a.U, o = q - k * a.U;
+    // the <= CK_Q frames' M are independent loads: issue them with the checkpoint's,
+    // then step (frames past p read as M = 0, the identity step)
+    const int32_t n = p - q;
+    double m[CK_Q];
+#pragma unroll
+    for (int j = 0; j < CK_Q; ++j) m[j] = a.Mc[b][cm_index(a, c, q + min(j, max(n - 1, 0)))];
     double att = a.ck[b][(int64_t)(o / CK_Q) * a.RS + cm_col(a, c * a.SPC + k)];
-    for (int32_t i = q; i < p; ++i) att = comp_step(att, a.Mc[b][cm_index(a, c, i)], bs);
+#pragma unroll
+    for (int j = 0; j < CK_Q; ++j) att = comp_step(att, j < n ? m[j] : 0.0, bs);
     return att;
 }
 
@@ -570,7 +604,10 @@ __device__ __forceinline__ double neg_div20(double att) {
     return fma(rem, 0.05, q);
 }
 
-__global__ void __launch_bounds__(192) comp_apply_kernel(CompArgs a) {
+#ifndef MM_APPLY_MINB
+#define MM_APPLY_MINB 1
+#endif
+__global__ void __launch_bounds__(192, MM_APPLY_MINB) comp_apply_kernel(CompArgs a) {
     constexpr int S = APPLY_STEP;
     __shared__ short2 lds[3][S][APPLY_TILES];
     const int b = threadIdx.x / APPLY_TILES;

@@ -371,8 +371,10 @@ __global__ void __launch_bounds__(LB_THREADS, 4) xover_kernel(XoArgs a, LbArgs l
 
 // ----------------------------------------------------------- K-weighting stage
 struct KwArgs {
-    int64_t N_proc, G;
+    int64_t N_proc, G;     // G sub-tiles of T frames (T divides the mix's tile Tt)
     int T, ch;
+    int64_t Gt;            // tiles of the tile-major mix (its row stride)
+    int sub;               // sub-tiles per tile (Tt = sub * T)
     double sos[2][5];
     const int16_t *mix;     // tile-major int16 pairs (pre-gain chain output)
     int64_t n_segs;
@@ -385,14 +387,18 @@ struct KwArgs {
 // pyloudnorm Meter (AME:213-218): mono = f32 mean(L,R) (== (L+R)/65536 exactly),
 // high_shelf lfilter in f64 stored back to f32, high_pass lfilter in f64 stored
 // to f32, then squared sums per 0.4 s / 0.1 s block.  The whole track is one line.
+// A lane runs one (sub-)tile of T = Tt / sub frames of a mix tile; the chain uses
+// sub = 1 (5 sub-tiles per tile measured 2x slower: 5x the look-back blocks and
+// 5-line mix loads), the operator path any tile its tables were made for.
 template <bool P2>
 __device__ __forceinline__ void kw_pass(const KwArgs &a, int64_t g, int len, double (&z)[2][2], int64_t seg_end,
                                         double &e0, double &e1) {
-    const int64_t G = a.G;
-    const short2 *mix = reinterpret_cast<const short2 *>(a.mix);
+    const int64_t gt = g / a.sub;  // the mix tile holding sub-tile g, and its first row
+    const short2 *mix = reinterpret_cast<const short2 *>(a.mix) + (g - gt * a.sub) * a.T * a.Gt + gt;
+    const int64_t Gt = a.Gt;
     int64_t pf = g * a.T;
     stream<8, 3, short2>(
-        len, [&](int i) { return mix[(int64_t)min(i, len - 1) * G + g]; },
+        len, [&](int i) { return mix[(int64_t)min(i, len - 1) * Gt]; },
         [&](short2 q) {
             const float m = a.ch == 2 ? ((float)q.x + (float)q.y) * (1.0f / 65536.0f)
                                       : (float)q.x * (1.0f / 32768.0f);

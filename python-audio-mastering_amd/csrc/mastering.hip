@@ -60,6 +60,8 @@ struct mm_ctx {
     CompArgs ca{};
     uint32_t comp_stamp = 0;  // stamp of the last queued fix-up sweep
     unsigned *comp_changed = nullptr;
+    char *ctl = nullptr;                // the chain's control block (setup_control)
+    uint32_t *ctl_claims = nullptr;     // its zeroed claim stamps
     int comp_iters = 0, comp_pending = 0;
     unsigned comp_nb = 0;
     // loudness on the device
@@ -242,6 +244,10 @@ static int validate(mm_ctx *c, const mm_job *j) {
     if (j->eq.nsec > 0 && j->eq.tpb != tpb) return set_err(c, MM_ERR_ARG, "eq tables built for %d tiles/block, need %d", j->eq.tpb, tpb);
     if (j->multiband_on && j->xover.tpb != tpb) return set_err(c, MM_ERR_ARG, "crossover tables built for %d tiles/block", j->xover.tpb);
     if (j->lufs_on && j->kweight.tpb != LB_THREADS) return set_err(c, MM_ERR_ARG, "K-weighting tables built for %d tiles/block", j->kweight.tpb);
+    if (j->eq.nsec > 0 && j->eq.tile != j->tile) return set_err(c, MM_ERR_ARG, "eq tables built for %d-frame tiles", j->eq.tile);
+    if (j->multiband_on && j->xover.tile != j->tile) return set_err(c, MM_ERR_ARG, "crossover tables built for %d-frame tiles", j->xover.tile);
+    if (j->lufs_on && j->kweight.tile != j->tile)
+        return set_err(c, MM_ERR_ARG, "K-weighting tables built for %d-frame tiles", j->kweight.tile);
     if (j->multiband_on) {
         if (j->xover.nsec != 4 || j->xover.nsec_branch0 != 2) return set_err(c, MM_ERR_ARG, "crossover must be 2+2 sections");
         for (int b = 0; b < 3; ++b) {
@@ -307,7 +313,8 @@ static int comp_sweeps(mm_ctx *c, int n) {
         ca.stamp = ++c->comp_stamp;
         ca.changed = c->comp_changed + k;
         const unsigned int *prevf = k > 0 ? c->comp_changed + (k - 1) : nullptr;
-        RET(launch(c, "comp_fix", comp_fix_kernel, dim3(blocks_for(NS, 64), 3), dim3(64), 0, ca, prevf));
+        if (ca.buf_ok) RET(launch(c, "comp_fix", comp_fix_kernel<true>, dim3(blocks_for(NS, 64), 3), dim3(64), 0, ca, prevf));
+        else RET(launch(c, "comp_fix", comp_fix_kernel<false>, dim3(blocks_for(NS, 64), 3), dim3(64), 0, ca, prevf));
     }
     c->comp_pending = n;
     return MM_OK;
@@ -323,6 +330,7 @@ static int comp_back(mm_ctx *c) {
 // Pinned readback block of one chain pass (offsets in bytes): look-back error
 // word, sweep flags, re-walked frame count, loudness + gain, per-chunk active counts.
 constexpr size_t RB_ERR = 0, RB_FLAGS = 16, RB_WALKED = 80, RB_LG = 96, RB_TOTALS = 128;
+static size_t rb_bytes(int64_t nch) { return RB_TOTALS + (size_t)12 * nch; }
 
 static int ensure_rb(mm_ctx *c, size_t bytes) {
     if (c->rb_cap >= bytes) return MM_OK;
@@ -336,21 +344,13 @@ static int ensure_rb(mm_ctx *c, size_t bytes) {
 
 static int64_t comp_chunks(const mm_ctx *c) { return c->comp_on ? c->ca.GS / c->ca.SPC : 0; }
 
-// Queue the D2H copies of everything the host checks after the chain (no sync).
+// Queue the D2H copy of everything the host checks after the chain (no sync): the
+// readback area of the control block, in ONE copy.
 static int queue_readback(mm_ctx *c, bool lufs) {
+    (void)lufs;
     const int64_t nch = comp_chunks(c);
-    RET(ensure_rb(c, RB_TOTALS + (size_t)12 * nch + 64));
-    char *rb = c->rb;
-    *reinterpret_cast<unsigned *>(rb + RB_ERR) = 0u;
-    if (c->lb_error) HIPCHK(c, hipMemcpyAsync(rb + RB_ERR, c->lb_error, 4, hipMemcpyDeviceToHost, c->stream));
-    if (c->comp_on && c->comp_pending)
-        HIPCHK(c, hipMemcpyAsync(rb + RB_FLAGS, c->comp_changed, c->comp_pending * sizeof(unsigned),
-                                 hipMemcpyDeviceToHost, c->stream));
-    if (lufs && c->gate_out) HIPCHK(c, hipMemcpyAsync(rb + RB_LG, c->gate_out, 16, hipMemcpyDeviceToHost, c->stream));
-    if (c->comp_on) {
-        HIPCHK(c, hipMemcpyAsync(rb + RB_TOTALS, c->ca.total[0], (size_t)12 * nch, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipMemcpyAsync(rb + RB_WALKED, c->ca.walked, 8, hipMemcpyDeviceToHost, c->stream));
-    }
+    RET(ensure_rb(c, rb_bytes(nch) + 64));
+    HIPCHK(c, hipMemcpyAsync(c->rb, c->ctl, rb_bytes(nch), hipMemcpyDeviceToHost, c->stream));
     return MM_OK;
 }
 
@@ -379,19 +379,35 @@ static int chain_check(mm_ctx *c, bool *converged) {
     return evaluate_chain(c, converged);
 }
 
-// Control words of the whole chain, zeroed by ONE memset: [0] look-back error,
-// [256..512) sweep flags + walked count, then the eq / crossover / K-weighting
-// look-back regions (each fresh until its first use).
-static int setup_control(mm_ctx *c, unsigned nblk) {
+// Super-tile geometry of the envelope solve: U active frames per super-tile,
+// SPC super-tiles reserved per chunk, nch chunks.
+static void comp_geometry(const mm_job *j, int64_t G, int *U, int64_t *SPC, int64_t *nch) {
+    const int K = j->tiles_per_chunk;
+    *U = std::max(16, std::min(j->comp_super, FIX_MAX_U));
+    *U -= *U % CK_Q;
+    *nch = (G + K - 1) / K;
+    *SPC = ((int64_t)K * j->tile + *U - 1) / *U;
+}
+
+// Control words of the whole chain, zeroed by ONE memset and read back by ONE
+// copy: the readback area (RB_* layout: look-back error word, sweep flags,
+// re-walked count, loudness + gain, per-chunk active counts), the sweeps' claim
+// stamps, then the eq / crossover / K-weighting look-back regions (each fresh
+// until its first use).
+static int setup_control(mm_ctx *c, unsigned nblk, int64_t nch, int64_t claims) {
     const size_t region = lb_flag_bytes(nblk);  // >= the K-weighting stage's (256 tiles per block)
-    const size_t bytes = 512 + 3 * region;
+    const size_t rba = (rb_bytes(nch) + 255) / 256 * 256, cla = ((size_t)claims * 4 + 255) / 256 * 256;
+    const size_t bytes = rba + cla + 3 * region;
     char *ctl;
     RET(get_buf(c, "ctl", bytes, &ctl));
     HIPCHK(c, hipMemsetAsync(ctl, 0, bytes, c->stream));
-    c->lb_error = reinterpret_cast<unsigned *>(ctl);
-    c->comp_changed = reinterpret_cast<unsigned *>(ctl + 256);
+    c->ctl = ctl;
+    c->lb_error = reinterpret_cast<unsigned *>(ctl + RB_ERR);
+    c->comp_changed = reinterpret_cast<unsigned *>(ctl + RB_FLAGS);
+    c->gate_out = reinterpret_cast<double *>(ctl + RB_LG);
+    c->ctl_claims = reinterpret_cast<uint32_t *>(ctl + rba);
     for (int r = 0; r < 3; ++r) {
-        c->ctl_lb[r] = reinterpret_cast<unsigned *>(ctl + 512 + r * region);
+        c->ctl_lb[r] = reinterpret_cast<unsigned *>(ctl + rba + cla + r * region);
         c->ctl_fresh[r] = true;
     }
     c->comp_flags_fresh = true;
@@ -415,10 +431,8 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     ca.K = K;
     ca.ch = ch;
     ca.warmup = j->comp_warmup;
-    ca.U = std::max(16, std::min(j->comp_super, FIX_MAX_U));
-    ca.U -= ca.U % CK_Q;
-    const int64_t nchunks = (G + K - 1) / K;
-    ca.SPC = ((int64_t)K * T + ca.U - 1) / ca.U;
+    int64_t nchunks;
+    comp_geometry(j, G, &ca.U, &ca.SPC, &nchunks);
     ca.GS = nchunks * ca.SPC;
     const int64_t NS = ca.GS;
     short2 *q2;
@@ -436,16 +450,16 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     uint32_t *claims;
     RET(get_buf(c, "comp_start", (size_t)3 * NS, &st));
     RET(get_buf(c, "comp_end", (size_t)3 * NS, &ends));
-    RET(get_buf(c, "comp_claim", (size_t)3 * NS, &claims));
-    HIPCHK(c, hipMemsetAsync(claims, 0, (size_t)3 * NS * sizeof(uint32_t), c->stream));
-    RET(get_buf(c, "comp_ck", (size_t)3 * RS * (ca.U / CK_Q + WALK_WB / CK_Q), &cks));  // + rows read ahead by re-walks
+    claims = c->ctl_claims;  // zeroed with the control block (sized by stage_front)
+    const int64_t ck_rows = ca.U / CK_Q + WALK_WB / CK_Q;  // + rows read ahead by re-walks
+    RET(get_buf(c, "comp_ck", (size_t)3 * RS * ck_rows, &cks));
     RET(get_buf(c, "comp_lut", (size_t)3 * 32769, &luts));
     unsigned int *changed = c->comp_changed;  // zeroed with the chain's control words
-    ca.walked = reinterpret_cast<unsigned long long *>(changed + 32);
+    ca.walked = reinterpret_cast<unsigned long long *>(c->ctl + RB_WALKED);
     int32_t *cnt, *off, *tot;
     RET(get_buf(c, "comp_cnt", (size_t)3 * G, &cnt));
     RET(get_buf(c, "comp_off", (size_t)3 * G, &off));
-    RET(get_buf(c, "comp_total", (size_t)3 * nchunks, &tot));
+    tot = reinterpret_cast<int32_t *>(c->ctl + RB_TOTALS);  // read back with the control block
     for (int b = 0; b < 3; ++b) {
         uint16_t *rb;
         double *mcb;
@@ -478,15 +492,21 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
         ca.off[b] = off + (size_t)b * G;
         ca.total[b] = tot + (size_t)b * nchunks;
         ca.start[b] = st + (size_t)b * NS;
-        ca.ck[b] = cks + (size_t)b * RS * (ca.U / CK_Q + WALK_WB / CK_Q);
+        ca.ck[b] = cks + (size_t)b * RS * ck_rows;
         ca.end[b] = ends + (size_t)b * NS;
         ca.claim[b] = claims + (size_t)b * NS;
     }
     RET(launch(c, "comp_rms", comp_rms_kernel, dim3(nb, 3), dim3(256), 0, ca));
     RET(launch(c, "comp_offsets", comp_offsets_kernel, dim3((unsigned)nchunks, 3), dim3(1024), 0, ca));
     RET(launch(c, "comp_compact", comp_compact_kernel, dim3(nb, 3), dim3(256), 0, ca));
-    RET(launch(c, "comp_pass0", comp_pass0_kernel,
-               dim3(blocks_for((NS + ca.own - 1) / ca.own, PASS0_BLOCK), 3), dim3(PASS0_BLOCK), 0, ca));
+    {
+        const size_t mcb = (size_t)RS * (ca.U + 1 + WALK_PAD) * sizeof(double), ckb = (size_t)RS * ck_rows * sizeof(double);
+        ca.buf_ok = mcb < ((size_t)1 << 31) && ckb < ((size_t)1 << 31) && !getenv("MM_FLAT_WALK");
+        ca.mc_bytes = ca.buf_ok ? (uint32_t)mcb : 0u;
+        ca.ck_bytes = ca.buf_ok ? (uint32_t)ckb : 0u;
+    }
+    const dim3 g0(blocks_for((NS + ca.own - 1) / ca.own, PASS0_BLOCK), 3);
+    RET(launch(c, "comp_pass0", comp_pass0_kernel, g0, dim3(PASS0_BLOCK), 0, ca));
     c->comp_on = true;
     c->ca = ca;
     c->comp_stamp = 0;
@@ -495,7 +515,7 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     c->comp_pending = 0;
     c->comp_nb = nb;
     int sweeps = COMP_SWEEPS;
-    if (const char *e = getenv("MM_COMP_SWEEPS")) sweeps = std::max(1, std::min(64, atoi(e)));  // tests / tuning
+    if (const char *e = getenv("MM_COMP_SWEEPS")) sweeps = std::max(1, std::min(16, atoi(e)));  // tests / tuning
     RET(comp_sweeps(c, sweeps));
     RET(comp_back(c));
     return MM_OK;
@@ -515,7 +535,12 @@ static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
     RET(get_buf(c, "q1", TG, &q1));
     const int tpb = LB_THREADS / ch;
     const unsigned nblk = blocks_for(std::max<int64_t>(G, 1), tpb);
-    RET(setup_control(c, nblk));
+    int64_t nch = 0, spc = 0;
+    if (j->multiband_on) {
+        int u;
+        comp_geometry(j, G, &u, &spc, &nch);
+    }
+    RET(setup_control(c, nblk, nch, 3 * nch * spc));
 
     EqArgs ea{};
     ea.in = j->in_kind == MM_IN_I16 ? nullptr : static_cast<const float *>(d_in);
@@ -649,6 +674,8 @@ static int kweight_launch(mm_ctx *c, const double *carry_in_host, double *line_e
     ka.N_proc = j->frames_proc;
     ka.G = G;
     ka.T = j->tile;
+    ka.Gt = G;  // one lane per mix tile (sub-tiles measured slower, iir.hip)
+    ka.sub = 1;
     ka.ch = j->channels;
     for (int s_ = 0; s_ < 2; ++s_)
         for (int k = 0; k < 5; ++k) ka.sos[s_][k] = j->kweight.sos[s_][k];
@@ -682,7 +709,7 @@ static int kweight_device(mm_ctx *c) {
     const mm_job *j = &c->job;
     double *seg;
     RET(kweight_launch(c, nullptr, nullptr, &seg));
-    RET(get_buf(c, "gate_out", 2, &c->gate_out));
+    // c->gate_out: in the control block's readback area (setup_control)
     GateArgs ga{};
     ga.n_blocks = j->n_blocks;
     ga.blk_s0 = c->blk_s0;

@@ -332,27 +332,28 @@ int check_dtype(mm_ctx *c, int dtype) {
     return MM_OK;
 }
 
-// natural [N][ch] host samples -> tile-major f64 on the device (T = OPS_TILE)
+// natural [N][ch] host samples -> tile-major f64 on the device (tiles of T frames:
+// the filter tables' tile, OPS_TILE or the K-weighting sub-tile)
 constexpr int OPS_TILE = 125;
 
-int upload_tile_major(mm_ctx *c, int dtype, const void *in, int64_t N, int ch, int64_t G, double **tm) {
+int upload_tile_major(mm_ctx *c, int dtype, const void *in, int64_t N, int ch, int64_t G, double **tm, int T) {
     const size_t in_bytes = (size_t)N * ch * dtype_size(dtype);
     char *din;
     RET(get_buf(c, "op_in", std::max<size_t>(in_bytes, 1), &din));
-    RET(get_buf(c, "op_tm", (size_t)std::max<int64_t>(G, 1) * OPS_TILE * ch, tm));
+    RET(get_buf(c, "op_tm", (size_t)std::max<int64_t>(G, 1) * T * ch, tm));
     if (in_bytes) HIPCHK(c, hipMemcpyAsync(din, in, in_bytes, hipMemcpyHostToDevice, c->stream));
     const unsigned nb = blocks_for(G, OPS_TILES);
-    const size_t lds = ((size_t)OPS_TILES * (OPS_TILE * ch + 1)) * sizeof(double);
+    const size_t lds = ((size_t)OPS_TILES * (T * ch + 1)) * sizeof(double);
     if (dtype == MM_F32) {
         if (ch == 2) return launch(c, "to_tile_major", to_tile_major_kernel<float, 2>, dim3(nb), dim3(256), lds,
-                                   (const float *)din, *tm, N, G, OPS_TILE);
+                                   (const float *)din, *tm, N, G, T);
         return launch(c, "to_tile_major", to_tile_major_kernel<float, 1>, dim3(nb), dim3(256), lds, (const float *)din,
-                      *tm, N, G, OPS_TILE);
+                      *tm, N, G, T);
     }
     if (ch == 2) return launch(c, "to_tile_major", to_tile_major_kernel<double, 2>, dim3(nb), dim3(256), lds,
-                               (const double *)din, *tm, N, G, OPS_TILE);
+                               (const double *)din, *tm, N, G, T);
     return launch(c, "to_tile_major", to_tile_major_kernel<double, 1>, dim3(nb), dim3(256), lds, (const double *)din,
-                  *tm, N, G, OPS_TILE);
+                  *tm, N, G, T);
 }
 
 template <int NS, int CH>
@@ -382,7 +383,7 @@ int iir_in_place(mm_ctx *c, const mm_iir *f, int64_t N, int ch, int64_t G, doubl
     IirOpArgs ia{};
     ia.N = N;
     ia.G = G;
-    ia.T = OPS_TILE;
+    ia.T = f->tile;
     for (int s = 0; s < 4; ++s)
         for (int k = 0; k < 5; ++k) ia.sos[s][k] = s < f->nsec ? f->sos[s][k] : 0.0;
     ia.in = tm;
@@ -506,20 +507,22 @@ static int sosfilt_common(mm_ctx *c, int dtype, const void *in, int64_t frames, 
     RET(check_dtype(c, dtype));
     HIPCHK(c, hipSetDevice(c->device));
     if (frames == 0) return MM_OK;
-    const int64_t G = (frames + OPS_TILE - 1) / OPS_TILE;
+    const int T = f->tile;
+    if (T < 1 || T > 512) return set_err(c, MM_ERR_ARG, "filter tables built for %d-frame tiles", T);
+    const int64_t G = (frames + T - 1) / T;
     double *tm;
-    RET(upload_tile_major(c, dtype, in, frames, channels, G, &tm));
+    RET(upload_tile_major(c, dtype, in, frames, channels, G, &tm, T));
     RET(iir_in_place(c, f, frames, channels, G, tm, round_f32, mix, dtype == MM_F32));
     double *dout;
     RET(get_buf(c, "op_out", (size_t)frames * channels, &dout));
     const unsigned nb = blocks_for(G, OPS_TILES);
-    const size_t lds = ((size_t)OPS_TILES * (OPS_TILE * channels + 1)) * sizeof(double);
+    const size_t lds = ((size_t)OPS_TILES * (T * channels + 1)) * sizeof(double);
     if (channels == 2)
         RET(launch(c, "from_tile_major", from_tile_major_kernel<2>, dim3(nb), dim3(256), lds, (const double *)tm, dout,
-                   frames, G, OPS_TILE));
+                   frames, G, T));
     else
         RET(launch(c, "from_tile_major", from_tile_major_kernel<1>, dim3(nb), dim3(256), lds, (const double *)tm, dout,
-                   frames, G, OPS_TILE));
+                   frames, G, T));
     HIPCHK(c, hipMemcpyAsync(out, dout, (size_t)frames * channels * 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     resolve_events(c);
@@ -552,7 +555,10 @@ int mm_op_compress_bands(mm_ctx *c, const mm_job *j, const int16_t *lo, const in
     c->G = G;
     c->job = *j;
     c->staged = false;
-    RET(setup_control(c, blocks_for(G, LB_THREADS / ch)));
+    int u;
+    int64_t spc, nch;
+    comp_geometry(j, G, &u, &spc, &nch);
+    RET(setup_control(c, blocks_for(G, LB_THREADS / ch), nch, 3 * nch * spc));
     const size_t bytes = (size_t)N * ch * 2;
     char *din;
     RET(get_buf(c, "host_in", 3 * bytes, &din));
@@ -609,11 +615,13 @@ int mm_op_loudness(mm_ctx *c, const mm_job *j, int dtype, const void *in, double
     if (j->kweight.nsec != 2 || j->kweight.tpb != LB_THREADS) return set_err(c, MM_ERR_ARG, "K-weighting tables");
     if (j->n_segs < 1 || !j->seg_bounds || !j->block_lo || !j->block_hi || j->n_blocks < 1)
         return set_err(c, MM_ERR_ARG, "missing loudness geometry");
+    const int T = j->kweight.tile;  // the K-weighting tables' (sub-)tile
+    if (T < 1 || T > 512) return set_err(c, MM_ERR_ARG, "K-weighting tables built for %d-frame tiles", T);
     for (int64_t s = 0; s + 1 < j->n_segs; ++s)
-        if (std::min<int64_t>(j->seg_bounds[s + 1], N) - j->seg_bounds[s] < OPS_TILE)
+        if (std::min<int64_t>(j->seg_bounds[s + 1], N) - j->seg_bounds[s] < T)
             return set_err(c, MM_ERR_ARG, "loudness segment shorter than a tile");
     HIPCHK(c, hipSetDevice(c->device));
-    const int64_t G = (N + OPS_TILE - 1) / OPS_TILE;
+    const int64_t G = (N + T - 1) / T;
     const size_t esz = dtype_size(dtype);
     double *tm;
     if (ch == 2) {  // mean(axis=1) on the device, then the mono line
@@ -627,17 +635,17 @@ int mm_op_loudness(mm_ctx *c, const mm_job *j, int dtype, const void *in, double
         pa.out = dmono;
         if (dtype == MM_F32) RET(launch(c, "op_mono", pointwise_kernel<PW_MONO, float>, dim3(pw_blocks(N)), dim3(256), 0, pa));
         else RET(launch(c, "op_mono", pointwise_kernel<PW_MONO, double>, dim3(pw_blocks(N)), dim3(256), 0, pa));
-        RET(get_buf(c, "op_tm", (size_t)G * OPS_TILE, &tm));
+        RET(get_buf(c, "op_tm", (size_t)G * T, &tm));
         const unsigned nb = blocks_for(G, OPS_TILES);
-        const size_t lds = ((size_t)OPS_TILES * (OPS_TILE + 1)) * sizeof(double);
+        const size_t lds = ((size_t)OPS_TILES * (T + 1)) * sizeof(double);
         if (dtype == MM_F32)
             RET(launch(c, "to_tile_major", to_tile_major_kernel<float, 1>, dim3(nb), dim3(256), lds,
-                       (const float *)dmono, tm, N, G, OPS_TILE));
+                       (const float *)dmono, tm, N, G, T));
         else
             RET(launch(c, "to_tile_major", to_tile_major_kernel<double, 1>, dim3(nb), dim3(256), lds,
-                       (const double *)dmono, tm, N, G, OPS_TILE));
+                       (const double *)dmono, tm, N, G, T));
     } else {
-        RET(upload_tile_major(c, dtype, in, N, 1, G, &tm));
+        RET(upload_tile_major(c, dtype, in, N, 1, G, &tm, T));
     }
     RET(iir_in_place(c, &j->kweight, N, 1, G, tm, dtype == MM_F32));
     // segment energies -> gating on the device (gate.hip)
@@ -655,7 +663,9 @@ int mm_op_loudness(mm_ctx *c, const mm_job *j, int dtype, const void *in, double
     KwArgs ka{};
     ka.N_proc = N;
     ka.G = G;
-    ka.T = OPS_TILE;
+    ka.T = T;
+    ka.Gt = G;
+    ka.sub = 1;
     ka.ch = 1;
     ka.n_segs = j->n_segs;
     ka.seg_bounds = c->seg_bounds_dev;

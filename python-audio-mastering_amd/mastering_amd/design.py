@@ -216,6 +216,9 @@ def transition_matrix(sections, branches):
 
 
 LB_THREADS = 256  # threads per block of the single-pass IIR kernels (csrc/lookback.h)
+
+
+
 TILE_POW, BLK_POW = 8, 65
 
 

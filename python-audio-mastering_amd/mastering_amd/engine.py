@@ -148,6 +148,7 @@ class Job:
         dst.nsec_branch0 = branches[0]
         dst.dim = 2 * len(sections)
         dst.tpb = tpb
+        dst.tile = int(tile)
         for s, sec in enumerate(sections):
             for k in range(5):
                 dst.sos[s][k] = float(sec[k])

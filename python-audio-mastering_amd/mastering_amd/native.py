@@ -27,7 +27,8 @@ c_int64_p = ctypes.POINTER(ctypes.c_int64)
 
 class MMIir(ctypes.Structure):
     _fields_ = [("nsec", ctypes.c_int32), ("nsec_branch0", ctypes.c_int32), ("dim", ctypes.c_int32),
-                ("tpb", ctypes.c_int32), ("sos", (ctypes.c_double * 5) * 4),
+                ("tpb", ctypes.c_int32), ("tile", ctypes.c_int32), ("_pad", ctypes.c_int32),
+                ("sos", (ctypes.c_double * 5) * 4),
                 ("phi_tile_pow", (ctypes.c_double * (MAX_DIM * MAX_DIM)) * TILE_POW),
                 ("phi_blk_pow", (ctypes.c_double * (MAX_DIM * MAX_DIM)) * BLK_POW)]
 
