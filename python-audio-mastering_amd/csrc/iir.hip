@@ -33,7 +33,11 @@ __device__ __forceinline__ int16_t quantize(double v) {
 // apply_saturation (AME:128-134), f32 throughout; no FMA contraction so the
 // rounding sequence matches numpy: keep*x + mix*tanh(x*drive).
 __device__ __forceinline__ float saturate(float x, const SatArgs &s) {
+#ifdef MM_ABLATE_TANH  // timing-only builds (tools/ablate.sh): the exciter without its tanh
+    float t = __fmul_rn(x, s.drive);
+#else
     float t = tanhf(__fmul_rn(x, s.drive));
+#endif
     return __fadd_rn(__fmul_rn(s.keep, x), __fmul_rn(s.mix, t));
 }
 

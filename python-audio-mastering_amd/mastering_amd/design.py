@@ -18,6 +18,7 @@ Reference anchors (worker/audio_mastering_engine.py = "AME"):
 from __future__ import annotations
 
 import functools
+import os
 import math
 
 import numpy as np
@@ -25,7 +26,8 @@ import scipy.signal
 
 MAX_DIM = 8
 CHUNK_MS = 30 * 1000  # AME:48
-DEFAULT_TILE = 125     # divides 30 s chunks at every rate that is a multiple of 25 Hz
+DEFAULT_TILE = int(os.environ.get("MM_TILE", "125"))  # divides 30 s chunks at every rate that is a multiple
+                                                     # of 25 Hz (MM_TILE: tuning experiments)
 OPS_TILE = 125         # tile of the per-stage operators' look-back tables (== OPS_TILE in csrc/ops.hip)
 
 EQ_KEYS = ("bass_boost", "mid_cut", "presence_boost", "treble_boost")
