@@ -63,6 +63,7 @@ struct mm_ctx {
     char *ctl = nullptr;                // the chain's control block (setup_control)
     uint32_t *ctl_claims = nullptr;     // its zeroed claim stamps
     int comp_iters = 0, comp_pending = 0;
+    int comp_hint = 0;  // sweeps the last converged solve of this context needed, + 1 (0: none yet)
     unsigned comp_nb = 0;
     // loudness on the device
     double *gate_out = nullptr;         // [2]: L, gain
@@ -301,7 +302,7 @@ static int launch_eq(mm_ctx *c, int nsec, int ch, unsigned nblk, const EqArgs &e
 // successor may be stale) and exits at once if sweep k-1 flagged nothing.
 // Convergence is checked at the chain's single sync (evaluate_chain); a rare
 // unconverged batch is extended there (MM_COMP_SWEEPS sets the queued count).
-constexpr int COMP_SWEEPS = 6;  // queued per chain; more resume from the host (more sweeps, then apply again)
+constexpr int COMP_SWEEPS = 6;  // queued by a context's first chain; later ones follow comp_hint
 
 static int comp_sweeps(mm_ctx *c, int n) {
     CompArgs &ca = c->ca;
@@ -367,6 +368,7 @@ static int evaluate_chain(mm_ctx *c, bool *converged) {
         c->comp_iters += k;
         *converged = k < c->comp_pending;
         c->comp_pending = 0;
+        if (*converged) c->comp_hint = std::max(2, std::min(16, c->comp_iters + 2));
         if (!*converged && c->comp_iters >= c->job.comp_max_iters)
             return set_err(c, MM_ERR_STATE, "compressor did not converge in %d sweeps", c->comp_iters);
     }
@@ -514,7 +516,9 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     c->comp_iters = 0;
     c->comp_pending = 0;
     c->comp_nb = nb;
-    int sweeps = COMP_SWEEPS;
+    // as many as the last solve on this context needed (+ 1 spare): a stream of similar
+    // batches queues no idle sweeps and rarely resumes from the host
+    int sweeps = c->comp_hint > 0 ? c->comp_hint : COMP_SWEEPS;
     if (const char *e = getenv("MM_COMP_SWEEPS")) sweeps = std::max(1, std::min(16, atoi(e)));  // tests / tuning
     RET(comp_sweeps(c, sweeps));
     RET(comp_back(c));
