@@ -17,6 +17,15 @@ namespace mm {
 // in-flight stores and drains register prefetch pipelines at every barrier.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// The value held by the partner lane (lane ^ 1) of a stereo lane pair: a DPP
+// quad_perm [1,0,3,2] move (VALU), not __shfl_xor's ds_bpermute LDS round trip.
+__device__ __forceinline__ int32_t pair_swap(int32_t v) { return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false); }
+__device__ __forceinline__ double pair_swap(double v) {
+    const int64_t b = __double_as_longlong(v);
+    const int32_t lo = pair_swap((int32_t)(b & 0xffffffff)), hi = pair_swap((int32_t)(b >> 32));
+    return __longlong_as_double(((int64_t)hi << 32) | (uint32_t)lo);
+}
+
 // Correctly rounded f32 square root (numpy's np.sqrt / x ** 0.5 on float32).
 // __fsqrt_rn lowers to v_sqrt_f32 (1 ulp) on gfx950; the f64 square root is
 // correctly rounded and rounding it to f32 is exact-safe (53 >= 2*24 + 2 bits).

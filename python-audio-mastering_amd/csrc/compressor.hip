@@ -178,6 +178,11 @@ constexpr int COMPACT_B = MM_COMPACT_B, COMPACT_NB = MM_COMPACT_NB;
 // Inactive frames store into this lane's own padding slot (row U of the array),
 // so every store is unconditional; the element index is 32-bit and advanced
 // with selects (no per-frame branch), keeping the load pipeline counted.
+// ONE_CROSS (U >= T, checked on the host): a tile's active frames cross at most
+// one super-tile boundary, so the element of its j-th active frame is
+// j*RS + (j < jb ? a0 : a1) — the only per-frame chain is j*RS += act*RS; the
+// general form below carries row, column and owner through a select chain.
+template <bool ONE_CROSS>
 __global__ void __launch_bounds__(256) comp_compact_kernel(CompArgs a) {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int b = blockIdx.y;
@@ -196,6 +201,22 @@ __global__ void __launch_bounds__(256) comp_compact_kernel(CompArgs a) {
     uint32_t idx = o * RS + col;  // its element
     const uint32_t dummy = U * RS + g32 % RS;
     double *Mc = a.Mc[b];
+    if constexpr (ONE_CROSS) {
+        const uint32_t jbRS = (U - o) * RS;  // j*RS at the boundary (row 0 of super-tile sg + 1)
+        const uint32_t sg1 = sg + 1, col1 = (sg1 % own) * ocols + sg1 / own;
+        const uint32_t a0 = idx, a1 = col1 - jbRS;  // mod 2^32: a1 + jbRS == col1
+        uint32_t jRS = 0;
+        stream2<COMPACT_B, COMPACT_NB, uint16_t, double>(
+            len, [&](int i) { return R[(uint32_t)min(i, len - 1) * G32]; },
+            [&](uint16_t r) { return lut[r]; },
+            [&](uint16_t r, double m) {
+                const bool act = (uint32_t)r >= r0;
+                const uint32_t e = jRS + (jRS < jbRS ? a0 : a1);
+                Mc[act ? e : dummy] = m;
+                jRS += act ? RS : 0u;
+            });
+        return;
+    }
     stream2<COMPACT_B, COMPACT_NB, uint16_t, double>(
         len, [&](int i) { return R[(uint32_t)min(i, len - 1) * G32]; },
         [&](uint16_t r) { return lut[r]; },

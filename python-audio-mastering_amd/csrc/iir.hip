@@ -156,7 +156,7 @@ __device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, doub
             for (int s = 0; s < NS; ++s) y = df2t(y, z[s][0], z[s][1], sos[s]);
             if (P2) {
                 if (CH == 2 && a.width_on) {  // apply_stereo_width (AME:136-144), f64
-                    const double o = __shfl_xor(y, 1);
+                    const double o = pair_swap(y);
                     const double yl = c == 0 ? y : o, yr = c == 0 ? o : y;
                     const double mid = (yl + yr) / 2;
                     const double side = (yl - yr) / 2 * a.width;
@@ -188,7 +188,7 @@ __device__ void eq_pass2(const EqArgs &a, int64_t g, int c, int len, double (&z)
 #pragma unroll
             for (int s = 0; s < NS; ++s) y = df2t(y, z[s][0], z[s][1], sos[s]);
             if (CH == 2 && a.width_on) {  // apply_stereo_width (AME:136-144), f64
-                const double o = __shfl_xor(y, 1);
+                const double o = pair_swap(y);
                 const double yl = c == 0 ? y : o, yr = c == 0 ? o : y;
                 const double mid = (yl + yr) / 2;
                 const double side = (yl - yr) / 2 * a.width;
@@ -293,11 +293,11 @@ struct XoArgs {
     int tail_from[3];
 };
 
-template <int CH>
-__device__ __forceinline__ double frame_energy2(int16_t q) {  // L^2 + R^2 of the lane pair (mono: q^2)
+// this lane's channel's q^2; the lane pair's sums are added once per tile (exact
+// integers below 2^53 in any order), so no per-frame lane exchange
+__device__ __forceinline__ double sample_energy(int16_t q) {
     const int32_t v = q;
-    const int32_t w = CH == 2 ? __shfl_xor(v, 1) : 0;
-    return (double)((uint32_t)(v * v) + (uint32_t)(w * w));
+    return (double)(uint32_t)(v * v);
 }
 
 template <int CH, bool P2>
@@ -327,13 +327,20 @@ __device__ __forceinline__ void xo_pass(const XoArgs &a, int64_t g, int c, int l
                 }
 #pragma unroll
                 for (int b = 0; b < 3; ++b) {
-                    const double e = frame_energy2<CH>(q[b]);
+                    const double e = sample_energy(q[b]);
                     E[b] += e;
                     tl[b] += pn >= a.tail_from[b] ? e : 0.0;
                 }
             }
             ++pn;
         });
+    if (P2 && CH == 2) {  // L^2 + R^2 sums of the lane pair
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            E[b] += pair_swap(E[b]);
+            tl[b] += pair_swap(tl[b]);
+        }
+    }
     if (P2 && c == 0) {
 #pragma unroll
         for (int b = 0; b < 3; ++b) {

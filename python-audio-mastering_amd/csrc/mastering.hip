@@ -500,7 +500,8 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     }
     RET(launch(c, "comp_rms", comp_rms_kernel, dim3(nb, 3), dim3(256), 0, ca));
     RET(launch(c, "comp_offsets", comp_offsets_kernel, dim3((unsigned)nchunks, 3), dim3(1024), 0, ca));
-    RET(launch(c, "comp_compact", comp_compact_kernel, dim3(nb, 3), dim3(256), 0, ca));
+    if (ca.U >= T) RET(launch(c, "comp_compact", comp_compact_kernel<true>, dim3(nb, 3), dim3(256), 0, ca));
+    else RET(launch(c, "comp_compact", comp_compact_kernel<false>, dim3(nb, 3), dim3(256), 0, ca));
     {
         const size_t mcb = (size_t)RS * (ca.U + 1 + WALK_PAD) * sizeof(double), ckb = (size_t)RS * ck_rows * sizeof(double);
         ca.buf_ok = mcb < ((size_t)1 << 31) && ckb < ((size_t)1 << 31) && !getenv("MM_FLAT_WALK");

@@ -31,16 +31,39 @@ __global__ void __launch_bounds__(256) casc(Sos s, int F, double *out) {
     }
     out[lane] = acc;
 }
+// the cascade skewed by one frame per section: section k runs frame i-k, so the
+// NS section updates of an iteration are independent (ILP) instead of a chain
 template <int NS, int SAT, int CHAINS>
+__global__ void __launch_bounds__(256) casc_skew(Sos s, int F, double *out) {
+    const int lane = blockIdx.x * blockDim.x + threadIdx.x;
+    double z[NS][2] = {};
+    double p[NS] = {};
+    double acc = 0;
+    float x0 = (float)(lane & 255) * 1e-3f;
+    for (int i = 0; i < F; ++i) {
+        float xf = x0 + (float)i * 1e-4f;
+        if (SAT) xf = 0.7f * xf + 0.3f * tanhf(xf * 2.2f);
+        p[0] = (double)xf;
+        double q[NS];
+#pragma unroll
+        for (int k = 0; k < NS; ++k) q[k] = df2t(p[k], z[k][0], z[k][1], s.c[k]);
+        acc += q[NS - 1] > 0.5 ? 1.0 : 0.0;
+#pragma unroll
+        for (int k = 1; k < NS; ++k) p[k] = q[k - 1];
+    }
+    out[lane] = acc;
+}
+template <int NS, int SAT, int CHAINS, bool SKEW = false>
 void run(const char *name, Sos s, double *d) {
     hipEvent_t a, b;
     hipEventCreate(&a); hipEventCreate(&b);
     const int F = 1000;
     for (int wps : {1, 2, 4, 8}) {  // waves per SIMD (256 CUs x 4 SIMDs)
         const int lanes = 256 * 4 * 64 * wps / CHAINS;
-        casc<NS, SAT, CHAINS><<<lanes / 256, 256>>>(s, F, d);
+        auto k = SKEW ? casc_skew<NS, SAT, CHAINS> : casc<NS, SAT, CHAINS>;
+        k<<<lanes / 256, 256>>>(s, F, d);
         hipEventRecord(a);
-        casc<NS, SAT, CHAINS><<<lanes / 256, 256>>>(s, F, d);
+        k<<<lanes / 256, 256>>>(s, F, d);
         hipEventRecord(b);
         hipEventSynchronize(b);
         float ms; hipEventElapsedTime(&ms, a, b);
@@ -57,5 +80,7 @@ int main() {
     run<4, 1, 1>("4 sections + tanhf", s, d);
     run<4, 0, 2>("4 sections x2 chains", s, d);
     run<2, 0, 1>("2 sections", s, d);
+    run<4, 0, 1, true>("4 sections skewed", s, d);
+    run<4, 1, 1, true>("4 sections skewed+tanhf", s, d);
     return 0;
 }
