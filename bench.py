@@ -6,7 +6,9 @@ the rank's share once, inputs and outputs resident in HBM):
       config).  With N > 1 every rank masters its own track: file sharding, no
       data-path collective, "scaling": "weak".
   C3  8 x 3-min 44.1 kHz tracks per GPU (64 tracks over 8 GPUs), file-sharded,
-      run as one mm_master_batch (up to 8 tracks in flight on their own streams).
+      run as one mm_master_batch: same-settings tracks fused into one timeline
+      (units of <= 72 M frames, every stage launched once per unit), units in
+      flight on their own streams.
   C4  one 2-h 44.1 kHz track time-sharded over the N ranks: each rank stages its
       contiguous 30 s chunks, then the K-weighting carry all-gather and ONE sum
       all-reduce of the 0.1 s loudness energies run through the library's own RCCL
@@ -206,9 +208,13 @@ class Runner:
         else:
             tracks = wl["tracks"]
             self.jobs, self.xs, self.outs = [], [], []
+            # the batch's tracks back to back in one device buffer (per-track views): a
+            # fused unit of whole-chunk tracks then reads them in place (mm_master_batch)
+            self.x_all = torch.empty((tracks * frames, 2), dtype=torch.float32, device=self.dev)
             for t in range(tracks):
                 pcm = pink_noise_pcm16(frames, rate, 2, track=rank * tracks + t)
-                self.xs.append(torch.from_numpy(pcm.astype(np.float32) / 32768).to(self.dev))
+                self.x_all[t * frames:(t + 1) * frames].copy_(torch.from_numpy(pcm.astype(np.float32) / 32768))
+                self.xs.append(self.x_all[t * frames:(t + 1) * frames])
                 job = Job(frames, rate, 2, params, out_kind=out_kind)
                 self.jobs.append(job)
                 self.outs.append(torch.empty((job.frames_proc, 2), dtype=torch.float32, device=self.dev))

@@ -148,12 +148,13 @@ struct CompArgs {
     int32_t *cnt[3];           // per tile: active frames
     int32_t *off[3];           // per tile: compacted index of its first active frame (in chunk)
     int32_t *total[3];         // per chunk: active frames
-    double *Mc[3];             // compacted M of active frames, super-tile-major [U + 1][GS]
+    double *Mc[3];             // compacted M of active frames, chunk blocks [chunk][U + 1 + pad][RS]
     double *ck[3];             // envelope checkpoints: state on entry to compacted rows o = 0, Q, 2Q, ...
                                // of every super-tile, [U / Q][GS] (written by the owning walks)
     int own;                   // super-tiles walked per pass-0 lane (after one warm-up)
-    int64_t ocols;             // ceil(GS / own): pass-0 lanes per band
-    int64_t RS;                // row stride of Mc / ck (own * ocols >= GS columns)
+    int64_t ocols;             // ceil(SPC / own): pass-0 lanes per chunk and band
+    int64_t RS;                // row stride of a chunk's block of Mc / ck (own * ocols >= SPC columns)
+    int64_t CB, CKB;           // elements of one chunk's block of Mc ([U + 1 + pad][RS]) and of ck
     uint32_t mc_bytes, ck_bytes;  // bytes of one band's Mc / ck (buffer descriptors)
     int buf_ok;                // both under 2 GB: walks use buffer loads (compressor.hip ColWalk)
     double *start[3];          // per-super-tile start state
@@ -166,7 +167,8 @@ struct CompArgs {
 };
 
 struct FinArgs {
-    int64_t N_proc, G;
+    int64_t N_proc, G;       // frames and tiles of this track
+    int64_t Gs, g_off;       // row stride of the tile-major mix, this track's first tile in it
     int T, ch, out_kind, use_gain;
     double gain;
     const double *gain_dev;  // device gain (loudness gated on the device) or null

@@ -19,7 +19,7 @@
 //                  tile's active-frame count;
 //  2. comp_offsets per (chunk, band): exclusive scan of the counts;
 //  3. comp_compact per (tile, band): M of every active frame, scattered into
-//                  the compacted super-tile-major array Mc[U][GS];
+//                  the compacted super-tile-major array (per chunk: [U][SPC]);
 //  4. comp_pass0   per super-tile: warm-up walk over the previous super-tile
 //                  from att = 0, then its own walk -> start, end (exact for the
 //                  first super-tile of a chunk, where att starts at 0);
@@ -155,12 +155,20 @@ __global__ void __launch_bounds__(1024) comp_offsets_kernel(CompArgs a) {
     if (tid == 1023) a.total[b][blockIdx.x] = buf[1023];
 }
 
-// Column of super-tile s in Mc / ck: pass-0 lane j owns super-tiles j*own ..
-// j*own + own-1, so super-tile j*own + t lives in column t*ocols + j and the 64
-// lanes of a wave touch 64 consecutive columns (512 contiguous bytes) at every
-// step of every walk, whatever `own` is.
+// Column of super-tile s (chunk c, index k in it) in Mc / ck.  Every chunk has a
+// block of its own (rows RS elements apart: a walk's rows stay within a few MB,
+// where one track-wide array put them a whole band-width apart and its walks and
+// scatters missed the TLB on big batches).  Pass-0 lane j of a chunk owns its
+// super-tiles j*own .. j*own + own-1, so super-tile j*own + t lives in column
+// t*ocols + j and the 64 lanes of a wave touch 64 consecutive columns (512
+// contiguous bytes) at every step of every walk, whatever `own` is.
 __device__ __forceinline__ int64_t cm_col(const CompArgs &a, int64_t s) {
-    return (s % a.own) * a.ocols + s / a.own;
+    const int64_t c = s / a.SPC, k = s - c * a.SPC;
+    return c * a.CB + (k % a.own) * a.ocols + k / a.own;
+}
+__device__ __forceinline__ int64_t ck_col(const CompArgs &a, int64_t s) {
+    const int64_t c = s / a.SPC, k = s - c * a.SPC;
+    return c * a.CKB + (k % a.own) * a.ocols + k / a.own;
 }
 
 #ifndef MM_COMPACT_B
@@ -196,14 +204,14 @@ __global__ void __launch_bounds__(256) comp_compact_kernel(CompArgs a) {
     const int len = (int)min((int64_t)a.T, a.N_proc - g * a.T);
     const uint32_t p = (uint32_t)a.off[b][g];
     uint32_t k = p / U, o = p - k * U;  // super-tile and row of the next active frame
-    const uint32_t base = (uint32_t)(g / a.K) * (uint32_t)a.SPC;
-    uint32_t sg = base + k, t = sg % own, col = t * ocols + sg / own;  // its super-tile, column
+    const uint32_t cb = (uint32_t)(g / a.K) * (uint32_t)a.CB;  // the chunk's block
+    uint32_t t = k % own, col = cb + t * ocols + k / own;  // column of its super-tile
     uint32_t idx = o * RS + col;  // its element
-    const uint32_t dummy = U * RS + g32 % RS;
+    const uint32_t dummy = cb + U * RS + g32 % RS;
     double *Mc = a.Mc[b];
     if constexpr (ONE_CROSS) {
         const uint32_t jbRS = (U - o) * RS;  // j*RS at the boundary (row 0 of super-tile sg + 1)
-        const uint32_t sg1 = sg + 1, col1 = (sg1 % own) * ocols + sg1 / own;
+        const uint32_t k1 = k + 1, col1 = cb + (k1 % own) * ocols + k1 / own;  // (unused past the chunk's last)
         const uint32_t a0 = idx, a1 = col1 - jbRS;  // mod 2^32: a1 + jbRS == col1
         uint32_t jRS = 0;
         stream2<COMPACT_B, COMPACT_NB, uint16_t, double>(
@@ -365,9 +373,8 @@ __device__ __forceinline__ double comp_walk(double att, const CompArgs &a, int b
     constexpr int WB = WALK_WB, WP = 4;
     if (len <= 0) return att;
     // column s, rows RS apart; loads run up to WB rows past the end (padding rows)
-    const int64_t cs = cm_col(a, s);
-    ColWalk<BUF> pl(a.Mc[b], cs, a.RS, a.mc_bytes);
-    ColWalk<BUF> pc(CK ? a.ck[b] : a.Mc[b], cs, a.RS, a.ck_bytes);  // checkpoint rows
+    ColWalk<BUF> pl(a.Mc[b], cm_col(a, s), a.RS, a.mc_bytes);
+    ColWalk<BUF> pc(CK ? a.ck[b] : a.Mc[b], CK ? ck_col(a, s) : 0, a.RS, a.ck_bytes);  // checkpoint rows
     double buf[WB], inc[WP], dec[WP];
 #pragma unroll
     for (int k = 0; k < WB; ++k) buf[k] = pl.ld();
@@ -417,8 +424,8 @@ __device__ __forceinline__ double comp_rewalk(double att, const CompArgs &a, int
     *coalesced = false;
     *nw = len;
     if (len <= 0) return att;
-    const int64_t cs = cm_col(a, s);
-    ColWalk<BUF> pl(a.Mc[b], cs, a.RS, a.mc_bytes);
+    const int64_t cs = ck_col(a, s);
+    ColWalk<BUF> pl(a.Mc[b], cm_col(a, s), a.RS, a.mc_bytes);
     ColWalk<BUF> pc(a.ck[b], cs, a.RS, a.ck_bytes);
     ColWalk<BUF> po(a.ck[b], cs, CKB * a.RS, a.ck_bytes);  // old checkpoint of the next block start (padding rows)
     double buf[WB], inc[WP], dec[WP];
@@ -485,13 +492,15 @@ constexpr int PASS0_BLOCK = MM_PASS0_BLOCK;
 // (flat column walks: the buffer-load form measured slower here, 0.27 -> 0.30 ms on
 // C2, though it helps the sweeps' lone walkers)
 __global__ void __launch_bounds__(PASS0_BLOCK) comp_pass0_kernel(CompArgs a) {
-    const int64_t s0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * a.own;
+    const int64_t L = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // lane j of chunk c
     const int b = blockIdx.y;
-    if (s0 >= a.GS) return;
+    const int64_t c = L / a.ocols, j = L - c * a.ocols;
+    if (c * a.SPC >= a.GS) return;
+    const int64_t s0 = c * a.SPC + j * a.own, s1 = c * a.SPC + min(j * a.own + a.own, a.SPC);
     const BandStep bs = band_step(a, b);
     double att = 0.0;
     bool warm = false;
-    for (int64_t s = s0; s < min(s0 + a.own, a.GS); ++s) {
+    for (int64_t s = s0; s < s1; ++s) {
         const Super st = super_of(a, b, s);
         if (st.len == 0) {
             warm = false;
@@ -595,7 +604,7 @@ __device__ __forceinline__ double comp_state_at(const CompArgs &a, int b, int64_
     double m[CK_Q];
 #pragma unroll
     for (int j = 0; j < CK_Q; ++j) m[j] = a.Mc[b][cm_index(a, c, q + min(j, max(n - 1, 0)))];
-    double att = a.ck[b][(int64_t)(o / CK_Q) * a.RS + cm_col(a, c * a.SPC + k)];
+    double att = a.ck[b][(int64_t)(o / CK_Q) * a.RS + ck_col(a, c * a.SPC + k)];
 #pragma unroll
     for (int j = 0; j < CK_Q; ++j) att = comp_step(att, j < n ? m[j] : 0.0, bs);
     return att;

@@ -25,6 +25,8 @@ struct GateArgs {
     double scale;           // 1 / (0.4 rate)
     double target;          // LUFS target
     double *out;            // [0] = L, [1] = gain
+    const int64_t *trk_blk; // fused batch: block b gates track b's blocks [trk_blk[b], trk_blk[b+1])
+                            // into out[2b], out[2b+1]; null: one track, blocks [0, n_blocks)
 };
 
 constexpr int GATE_THREADS = 1024;
@@ -57,9 +59,12 @@ __global__ void __launch_bounds__(GATE_THREADS) gate_kernel(GateArgs a) {
     __shared__ double rs[GATE_THREADS];
     __shared__ long long rc[GATE_THREADS];
     const int t = threadIdx.x;
+    const int64_t j0 = a.trk_blk ? a.trk_blk[blockIdx.x] : 0;
+    const int64_t j1 = a.trk_blk ? a.trk_blk[blockIdx.x + 1] : a.n_blocks;
+    double *out = a.out + 2 * blockIdx.x;
     double sum = 0.0;
     long long cnt = 0;
-    for (int64_t j = t; j < a.n_blocks; j += GATE_THREADS) {
+    for (int64_t j = j0 + t; j < j1; j += GATE_THREADS) {
         const double z = gate_block_z(a, j);
         if (-0.691 + 10.0 * log10(z) >= -70.0) {
             sum += z;
@@ -71,7 +76,7 @@ __global__ void __launch_bounds__(GATE_THREADS) gate_kernel(GateArgs a) {
     const double gamma_r = -0.691 + 10.0 * log10(mean_abs) - 10.0;
     sum = 0.0;
     cnt = 0;
-    for (int64_t j = t; j < a.n_blocks; j += GATE_THREADS) {
+    for (int64_t j = j0 + t; j < j1; j += GATE_THREADS) {
         const double z = gate_block_z(a, j);
         const double l = -0.691 + 10.0 * log10(z);
         if (l > gamma_r && l > -70.0) {
@@ -83,8 +88,8 @@ __global__ void __launch_bounds__(GATE_THREADS) gate_kernel(GateArgs a) {
     if (t == 0) {
         const double zavg = cnt ? sum / (double)cnt : 0.0;
         const double L = -0.691 + 10.0 * log10(zavg);
-        a.out[0] = L;
-        a.out[1] = pow(10.0, (a.target - L) / 20.0);
+        out[0] = L;
+        out[1] = pow(10.0, (a.target - L) / 20.0);
     }
 }
 

@@ -393,6 +393,13 @@ struct KwArgs {
     double *part;           // [G][2] energies of the (at most two) segments a tile touches
     int64_t *part_seg;      // [G]   first segment of the tile
     double *line_end;       // optional [4]: state after the last frame
+    // fused batch (several tracks on one timeline, each starting at a chunk
+    // boundary): n_trk > 0 gives each track's first tile (its K-weighting line
+    // restarts there) and the end of its real frames (later frames of its last
+    // chunk are padding: zero energy).  n_trk == 0: one line from tile 0.
+    int n_trk;
+    const int64_t *trk_tile0;  // [n_trk] ascending
+    const int64_t *trk_end;    // [n_trk] timeline frame
 };
 
 // pyloudnorm Meter (AME:213-218): mono = f32 mean(L,R) (== (L+R)/65536 exactly),
@@ -403,7 +410,7 @@ struct KwArgs {
 // 5-line mix loads), the operator path any tile its tables were made for.
 template <bool P2>
 __device__ __forceinline__ void kw_pass(const KwArgs &a, int64_t g, int len, double (&z)[2][2], int64_t seg_end,
-                                        double &e0, double &e1) {
+                                        int64_t e_end, double &e0, double &e1) {
     const int64_t gt = g / a.sub;  // the mix tile holding sub-tile g, and its first row
     const short2 *mix = reinterpret_cast<const short2 *>(a.mix) + (g - gt * a.sub) * a.T * a.Gt + gt;
     const int64_t Gt = a.Gt;
@@ -418,7 +425,7 @@ __device__ __forceinline__ void kw_pass(const KwArgs &a, int64_t g, int len, dou
             const double y2 = df2t((double)y1f, z[1][0], z[1][1], a.sos[1]);
             if (P2) {
                 const float y2f = (float)y2;
-                const double e = (double)y2f * (double)y2f;
+                const double e = pf < e_end ? (double)y2f * (double)y2f : 0.0;
                 if (pf < seg_end) e0 += e;
                 else e1 += e;
             }
@@ -436,11 +443,23 @@ __global__ void __launch_bounds__(LB_THREADS, 2) kweight_kernel(KwArgs a, LbArgs
     const int len = valid ? (int)min((int64_t)a.T, a.N_proc - g * a.T) : 0;
     double zs[2][2] = {{0.0, 0.0}, {0.0, 0.0}};
     double e0 = 0.0, e1 = 0.0;
-    if (valid) kw_pass<false>(a, g, len, zs, 0, e0, e1);
+    // this tile's track (fused batch): its line start and real-frame end
+    int64_t line0 = 0, e_end = INT64_MAX;
+    if (a.n_trk > 0 && valid) {
+        int lo = 0, hi = a.n_trk;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (a.trk_tile0[mid] <= g) lo = mid;
+            else hi = mid;
+        }
+        line0 = a.trk_tile0[lo];
+        e_end = a.trk_end[lo];
+    }
+    if (valid) kw_pass<false>(a, g, len, zs, 0, e_end, e0, e1);
     double z[4] = {zs[0][0], zs[0][1], zs[1][0], zs[1][1]}, s[4], rst[4];
 #pragma unroll
     for (int d = 0; d < 4; ++d) rst[d] = lb.init ? lb.init[d] : 0.0;
-    lb_carry<4, 1>(lb, blk, t, 0, valid, valid && g == 0, rst, z, s, smem);
+    lb_carry<4, 1>(lb, blk, t, 0, valid, valid && g == line0, rst, z, s, smem);
     if (!valid) return;
     // loudness segment of the tile's first frame (largest s with bounds[s] <= f0)
     const int64_t f0 = g * a.T;
@@ -454,7 +473,7 @@ __global__ void __launch_bounds__(LB_THREADS, 2) kweight_kernel(KwArgs a, LbArgs
     zs[0][1] = s[1];
     zs[1][0] = s[2];
     zs[1][1] = s[3];
-    kw_pass<true>(a, g, len, zs, a.seg_bounds[lo + 1], e0, e1);
+    kw_pass<true>(a, g, len, zs, a.seg_bounds[lo + 1], e_end, e0, e1);
     a.part[2 * g] = e0;
     a.part[2 * g + 1] = e1;
     a.part_seg[g] = lo;

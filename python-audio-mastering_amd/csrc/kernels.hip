@@ -62,7 +62,7 @@ __global__ void __launch_bounds__(256) finalize_kernel(FinArgs a) {
     const int ntile = (int)min((int64_t)FIN_TILES, a.G - g0);
     for (int i = threadIdx.x; i < T * FIN_TILES; i += blockDim.x) {
         const int n = i / FIN_TILES, t = i % FIN_TILES;
-        if (t < ntile) lds[t * stride + n] = a.mix[(int64_t)n * a.G + g0 + t];
+        if (t < ntile) lds[t * stride + n] = a.mix[(int64_t)n * a.Gs + a.g_off + g0 + t];
     }
     __syncthreads();
     const int64_t f_base = g0 * T;

@@ -445,7 +445,7 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     // more per lane on bigger problems and when batch streams run beside this one
     ca.own = c->own_override > 0 ? c->own_override
                                  : (int)std::max<int64_t>(1, std::min<int64_t>(4, (NS * c->concurrency + 3307) / 6615));
-    ca.ocols = (NS + ca.own - 1) / ca.own;
+    ca.ocols = (ca.SPC + ca.own - 1) / ca.own;
     ca.RS = ca.ocols * ca.own;
     const int64_t RS = ca.RS;
     double *st, *ends, *luts, *cks;
@@ -454,7 +454,9 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     RET(get_buf(c, "comp_end", (size_t)3 * NS, &ends));
     claims = c->ctl_claims;  // zeroed with the control block (sized by stage_front)
     const int64_t ck_rows = ca.U / CK_Q + WALK_WB / CK_Q;  // + rows read ahead by re-walks
-    RET(get_buf(c, "comp_ck", (size_t)3 * RS * ck_rows, &cks));
+    ca.CB = RS * (ca.U + 1 + WALK_PAD);  // + compaction dummy row + walk prefetch rows
+    ca.CKB = RS * ck_rows;
+    RET(get_buf(c, "comp_ck", (size_t)3 * nchunks * ca.CKB, &cks));
     RET(get_buf(c, "comp_lut", (size_t)3 * 32769, &luts));
     unsigned int *changed = c->comp_changed;  // zeroed with the chain's control words
     ca.walked = reinterpret_cast<unsigned long long *>(c->ctl + RB_WALKED);
@@ -469,7 +471,7 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
         snprintf(nm, sizeof nm, "comp_r%d", b);
         RET(get_buf(c, nm, TG, &rb));
         snprintf(nm, sizeof nm, "comp_mc%d", b);
-        RET(get_buf(c, nm, (size_t)RS * (ca.U + 1 + WALK_PAD), &mcb));  // + compaction dummy row + walk prefetch rows
+        RET(get_buf(c, nm, (size_t)nchunks * ca.CB, &mcb));
         ca.r16[b] = rb;
         ca.E[b] = tile_e + (size_t)(2 * b) * G;
         ca.tail[b] = tile_e + (size_t)(2 * b + 1) * G;
@@ -494,7 +496,7 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
         ca.off[b] = off + (size_t)b * G;
         ca.total[b] = tot + (size_t)b * nchunks;
         ca.start[b] = st + (size_t)b * NS;
-        ca.ck[b] = cks + (size_t)b * RS * ck_rows;
+        ca.ck[b] = cks + (size_t)b * nchunks * ca.CKB;
         ca.end[b] = ends + (size_t)b * NS;
         ca.claim[b] = claims + (size_t)b * NS;
     }
@@ -503,12 +505,12 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     if (ca.U >= T) RET(launch(c, "comp_compact", comp_compact_kernel<true>, dim3(nb, 3), dim3(256), 0, ca));
     else RET(launch(c, "comp_compact", comp_compact_kernel<false>, dim3(nb, 3), dim3(256), 0, ca));
     {
-        const size_t mcb = (size_t)RS * (ca.U + 1 + WALK_PAD) * sizeof(double), ckb = (size_t)RS * ck_rows * sizeof(double);
+        const size_t mcb = (size_t)nchunks * ca.CB * sizeof(double), ckb = (size_t)nchunks * ca.CKB * sizeof(double);
         ca.buf_ok = mcb < ((size_t)1 << 31) && ckb < ((size_t)1 << 31) && !getenv("MM_FLAT_WALK");
         ca.mc_bytes = ca.buf_ok ? (uint32_t)mcb : 0u;
         ca.ck_bytes = ca.buf_ok ? (uint32_t)ckb : 0u;
     }
-    const dim3 g0(blocks_for((NS + ca.own - 1) / ca.own, PASS0_BLOCK), 3);
+    const dim3 g0(blocks_for(nchunks * ca.ocols, PASS0_BLOCK), 3);
     RET(launch(c, "comp_pass0", comp_pass0_kernel, g0, dim3(PASS0_BLOCK), 0, ca));
     c->comp_on = true;
     c->ca = ca;
@@ -768,6 +770,8 @@ static int finalize(mm_ctx *c, double gain, const double *gain_dev, int use_gain
     FinArgs fa{};
     fa.N_proc = j->frames_proc;
     fa.G = c->G;
+    fa.Gs = c->G;
+    fa.g_off = 0;
     fa.T = j->tile;
     fa.ch = j->channels;
     fa.out_kind = j->out_kind;
@@ -839,6 +843,301 @@ static int stage_chunks(mm_ctx *c, const mm_job *j, const void *d_in) {
     }
 }
 
+// ------------------------------------------------------------ fused batch
+// Tracks with the same settings mastered as ONE timeline (BASELINE C3/C5 on one
+// GPU).  Track i occupies whole chunks [off_i, off_i + n_i * CF) of it, its last
+// chunk zero-padded; every per-chunk stage (EQ, crossover, compressor: AME:48-77
+// restarts them per chunk) then runs once over all tracks with the single-track
+// kernels, and the padding changes none of a track's frames because it follows
+// them and every stage is causal.  The K-weighting line restarts at each track
+// start and gives padding frames zero energy; the gating runs one block per
+// track; finalize writes every track to its own output.  One launch per stage
+// covers the whole batch (n times one track's lanes), which fills the GPU where a
+// single track's latency-bound launches leave most SIMDs idle.
+struct FusedPlan {
+    std::vector<int64_t> off;  // [n + 1] first timeline frame of each track (and the end)
+    std::vector<int64_t> nch;  // [n] chunks of each track
+    int64_t P = 0;             // timeline frames
+    // loudness geometry on the device
+    int64_t n_segs = 0, n_blocks = 0;
+    int64_t *bounds = nullptr, *trk_blk = nullptr, *trk_tile0 = nullptr, *trk_end = nullptr;
+    int32_t *s0 = nullptr, *s1 = nullptr;
+};
+
+static bool same_iir(const mm_iir &a, const mm_iir &b) { return memcmp(&a, &b, sizeof a) == 0; }
+
+// jobs that differ only in their track (length, loudness geometry): one timeline
+static bool fusable(const mm_job *J, int n) {
+    const mm_job &a = J[0];
+    for (int i = 0; i < n; ++i) {
+        const mm_job &b = J[i];
+        if (b.frames_proc <= 0) return false;
+        if (i == 0) continue;
+        if (b.channels != a.channels || b.rate != a.rate || b.tile != a.tile || b.tiles_per_chunk != a.tiles_per_chunk ||
+            b.sat_keep != a.sat_keep || b.sat_mix != a.sat_mix || b.sat_drive != a.sat_drive || b.sat_on != a.sat_on ||
+            b.width != a.width || b.width_on != a.width_on || b.multiband_on != a.multiband_on ||
+            b.lufs_on != a.lufs_on || b.out_kind != a.out_kind || b.in_kind != a.in_kind ||
+            b.comp_warmup != a.comp_warmup || b.comp_max_iters != a.comp_max_iters || b.comp_super != a.comp_super)
+            return false;
+        if (!same_iir(a.eq, b.eq)) return false;
+        if (a.lufs_on && (b.lufs_target != a.lufs_target || b.block_scale != a.block_scale || !same_iir(a.kweight, b.kweight)))
+            return false;
+        if (a.multiband_on) {
+            if (!same_iir(a.xover, b.xover)) return false;
+            for (int k = 0; k < 3; ++k) {
+                const mm_band &x = a.band[k], &y = b.band[k];
+                if (x.thresh_rms != y.thresh_rms || x.attack_frames != y.attack_frames ||
+                    x.release_frames != y.release_frames || x.look != y.look || x.r0 != y.r0)
+                    return false;
+                if (x.lut != y.lut && memcmp(x.lut, y.lut, (size_t)32769 * 4 * sizeof(double)) != 0) return false;
+            }
+        }
+    }
+    return true;
+}
+
+static bool fused_layout(const mm_job *J, int n, FusedPlan *p) {
+    const int64_t CF = (int64_t)J[0].tile * J[0].tiles_per_chunk;
+    p->off.assign((size_t)n + 1, 0);
+    p->nch.assign((size_t)n, 0);
+    for (int i = 0; i < n; ++i) {
+        p->nch[i] = (J[i].frames_proc + CF - 1) / CF;
+        p->off[i + 1] = p->off[i] + p->nch[i] * CF;
+    }
+    p->P = p->off[n];
+    return p->P < ((int64_t)1 << 31);  // 32-bit frame indexing
+}
+
+// Loudness geometry of the timeline, uploaded before anything is queued (its one
+// sync then waits on nothing): every track's segment bounds shifted to its
+// offset (a bound shared with the previous track's end is not repeated; the gap
+// between a track's last bound and the next track start is a padding segment
+// no gating block reads), every track's blocks as segment ranges of that list.
+static int fused_geometry(mm_ctx *c, const mm_job *J, int n, FusedPlan *p) {
+    const int T = J[0].tile;
+    std::vector<int64_t> bounds, tblk((size_t)n + 1), tt0((size_t)n), tend((size_t)n);
+    std::vector<int32_t> s0, s1;
+    for (int i = 0; i < n; ++i) {
+        const mm_job &j = J[i];
+        const int64_t o = p->off[i];
+        int64_t base;
+        if (!bounds.empty() && bounds.back() == o + j.seg_bounds[0]) {
+            base = (int64_t)bounds.size() - 1;
+        } else {
+            base = (int64_t)bounds.size();
+            bounds.push_back(o + j.seg_bounds[0]);
+        }
+        for (int64_t s = 1; s <= j.n_segs; ++s) bounds.push_back(o + j.seg_bounds[s]);
+        tblk[i] = (int64_t)s0.size();
+        const int64_t *B = j.seg_bounds, S = j.n_segs;
+        for (int64_t b = 0; b < j.n_blocks; ++b) {  // as mm_gate_loudness
+            s0.push_back((int32_t)(base + std::min<int64_t>(std::lower_bound(B, B + S + 1, j.block_lo[b]) - B, S)));
+            s1.push_back((int32_t)(base + std::min<int64_t>(std::lower_bound(B, B + S + 1, j.block_hi[b]) - B, S)));
+        }
+        tt0[i] = o / T;
+        tend[i] = o + j.frames_proc;
+    }
+    tblk[n] = (int64_t)s0.size();
+    if (bounds.back() < p->P) bounds.push_back(p->P);  // the last track's padding
+    p->n_segs = (int64_t)bounds.size() - 1;
+    p->n_blocks = (int64_t)s0.size();
+    RET(get_buf(c, "fz_bounds", bounds.size(), &p->bounds));
+    RET(get_buf(c, "fz_trk_blk", tblk.size(), &p->trk_blk));
+    RET(get_buf(c, "fz_trk_tile0", tt0.size(), &p->trk_tile0));
+    RET(get_buf(c, "fz_trk_end", tend.size(), &p->trk_end));
+    RET(get_buf(c, "fz_s0", std::max<size_t>(s0.size(), 1), &p->s0));
+    RET(get_buf(c, "fz_s1", std::max<size_t>(s1.size(), 1), &p->s1));
+    HIPCHK(c, hipMemcpyAsync(p->bounds, bounds.data(), bounds.size() * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(p->trk_blk, tblk.data(), tblk.size() * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(p->trk_tile0, tt0.data(), tt0.size() * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(p->trk_end, tend.data(), tend.size() * 8, hipMemcpyHostToDevice, c->stream));
+    if (!s0.empty()) {
+        HIPCHK(c, hipMemcpyAsync(p->s0, s0.data(), s0.size() * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(p->s1, s1.data(), s1.size() * 4, hipMemcpyHostToDevice, c->stream));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // host vectors are transient
+    return MM_OK;
+}
+
+// K-weighting (a line per track), segment energies and per-track gating into
+// lg[2i] = L, lg[2i+1] = gain.
+static int fused_loudness(mm_ctx *c, const mm_job &j0, int n, const FusedPlan &p, double *lg) {
+    const int64_t G = c->G;
+    double *part, *seg;
+    int64_t *part_seg;
+    RET(get_buf(c, "kw_part", (size_t)G * 2, &part));
+    RET(get_buf(c, "kw_part_seg", (size_t)G, &part_seg));
+    RET(get_buf(c, "kw_seg", (size_t)p.n_segs, &seg));
+    LbArgs lb{};
+    RET(upload_tables(c, "kweight", j0.kweight, lb));
+    const unsigned nblk = blocks_for(G, LB_THREADS);
+    RET(lb_prepare(c, nblk, 1, lb, 2));
+    KwArgs ka{};
+    ka.N_proc = p.P;
+    ka.G = G;
+    ka.T = j0.tile;
+    ka.Gt = G;
+    ka.sub = 1;
+    ka.ch = j0.channels;
+    for (int s_ = 0; s_ < 2; ++s_)
+        for (int k = 0; k < 5; ++k) ka.sos[s_][k] = j0.kweight.sos[s_][k];
+    ka.mix = reinterpret_cast<const int16_t *>(c->mix);
+    ka.n_segs = p.n_segs;
+    ka.seg_bounds = p.bounds;
+    ka.part = part;
+    ka.part_seg = part_seg;
+    ka.n_trk = n;
+    ka.trk_tile0 = p.trk_tile0;
+    ka.trk_end = p.trk_end;
+    RET(launch(c, "kweight", kweight_kernel, dim3(nblk), dim3(LB_THREADS), lb_lds_bytes<4, 1>(), ka, lb));
+    RET(launch(c, "seg_reduce", seg_reduce_kernel, dim3(blocks_for(p.n_segs, 4)), dim3(256), 0, ka, seg));
+    GateArgs ga{};
+    ga.n_blocks = p.n_blocks;
+    ga.blk_s0 = p.s0;
+    ga.blk_s1 = p.s1;
+    ga.seg = seg;
+    ga.scale = j0.block_scale;
+    ga.target = j0.lufs_target;
+    ga.out = lg;
+    ga.trk_blk = p.trk_blk;
+    return launch(c, "gate", gate_kernel, dim3((unsigned)n), dim3(GATE_THREADS), 0, ga);
+}
+
+static int fused_finalize(mm_ctx *c, const mm_job *J, int n, const FusedPlan &p, const double *lg, void *const *d_out) {
+    const mm_job &j0 = J[0];
+    const int T = j0.tile;
+    const size_t lds = (size_t)FIN_TILES * (T + 1) * sizeof(short2);
+    for (int i = 0; i < n; ++i) {
+        FinArgs fa{};
+        fa.N_proc = J[i].frames_proc;
+        fa.G = p.nch[i] * j0.tiles_per_chunk;
+        fa.Gs = c->G;
+        fa.g_off = p.off[i] / T;
+        fa.T = T;
+        fa.ch = j0.channels;
+        fa.out_kind = j0.out_kind;
+        fa.use_gain = j0.lufs_on;
+        fa.gain = 1.0;
+        fa.gain_dev = j0.lufs_on ? lg + 2 * i + 1 : nullptr;
+        fa.mix = c->mix;
+        fa.out = d_out[i];
+        const dim3 grid(blocks_for(fa.G, FIN_TILES));
+        if (fa.ch == 2) RET(launch(c, "finalize", finalize_kernel<2>, grid, dim3(256), lds, fa));
+        else RET(launch(c, "finalize", finalize_kernel<1>, grid, dim3(256), lds, fa));
+    }
+    return MM_OK;
+}
+
+// Queue a fused unit: loudness geometry (uploaded first: its sync waits on an
+// idle stream), the input timeline (in place when the tracks already lie back to
+// back on whole chunks, else gathered with the padding zeroed), the chunk stages,
+// loudness and the per-track finalize.
+static int fused_enqueue(mm_ctx *c, int n, const mm_job *J, const void *const *d_in, void *const *d_out, FusedPlan &p) {
+    const mm_job &j0 = J[0];
+    const bool lufs = j0.lufs_on != 0;
+    if (lufs) RET(fused_geometry(c, J, n, &p));
+    const size_t fb = (size_t)j0.channels * (j0.in_kind == MM_IN_I16 ? 2 : 4);
+    bool in_place = true;
+    for (int i = 0; i < n && in_place; ++i)
+        in_place = J[i].frames_in == p.off[i + 1] - p.off[i] &&
+                   static_cast<const char *>(d_in[i]) == static_cast<const char *>(d_in[0]) + p.off[i] * fb;
+    const void *tin = d_in[0];
+    if (!in_place) {
+        char *buf;
+        RET(get_buf(c, "fz_in", (size_t)p.P * fb, &buf));
+        for (int i = 0; i < n; ++i) {
+            const int64_t len = p.off[i + 1] - p.off[i], nin = std::min(J[i].frames_in, len);
+            if (nin > 0)
+                HIPCHK(c, hipMemcpyAsync(buf + p.off[i] * fb, d_in[i], nin * fb, hipMemcpyDeviceToDevice, c->stream));
+            if (len > nin) HIPCHK(c, hipMemsetAsync(buf + (p.off[i] + nin) * fb, 0, (len - nin) * fb, c->stream));
+        }
+        tin = buf;
+    }
+    mm_job tj = j0;  // the timeline as one job (loudness is per track)
+    tj.frames_in = tj.frames_proc = p.P;
+    tj.lufs_on = 0;
+    RET(stage_front(c, &tj, tin));
+    double *lg;
+    RET(get_buf(c, "fz_lg", (size_t)2 * n, &lg));
+    if (lufs) RET(fused_loudness(c, j0, n, p, lg));
+    RET(fused_finalize(c, J, n, p, lg, d_out));
+    return queue_readback(c, lufs);
+}
+
+static int fused_complete(mm_ctx *c, int n, const mm_job *J, void *const *d_out, mm_result *res, const FusedPlan &p) {
+    const mm_job &j0 = J[0];
+    const bool lufs = j0.lufs_on != 0;
+    double *lg;
+    RET(get_buf(c, "fz_lg", (size_t)2 * n, &lg));
+    for (;;) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        bool converged;
+        RET(evaluate_chain(c, &converged));
+        if (converged) break;
+        RET(comp_sweeps(c, 8));
+        RET(comp_back(c));
+        if (lufs) RET(fused_loudness(c, j0, n, p, lg));
+        RET(fused_finalize(c, J, n, p, lg, d_out));
+        RET(queue_readback(c, lufs));
+    }
+    if (!res) return MM_OK;
+    std::vector<double> l2((size_t)2 * n, 0.0);
+    if (lufs) HIPCHK(c, hipMemcpy(l2.data(), lg, l2.size() * sizeof(double), hipMemcpyDeviceToHost));
+    const int64_t nchk = comp_chunks(c), CF = (int64_t)j0.tile * j0.tiles_per_chunk;
+    const int32_t *tot = reinterpret_cast<const int32_t *>(c->rb + RB_TOTALS);
+    const int64_t walked = c->comp_on ? (int64_t) * reinterpret_cast<const unsigned long long *>(c->rb + RB_WALKED) : 0;
+    for (int i = 0; i < n; ++i) {
+        mm_result &r = res[i];
+        r.loudness = lufs ? l2[2 * i] : NAN;
+        r.gain_linear = lufs ? l2[2 * i + 1] : 1.0;
+        r.frames_out = J[i].frames_proc;
+        r.comp_iters = c->comp_iters;  // one solve for the whole unit
+        r.comp_active = 0;
+        for (int b = 0; b < 3 && c->comp_on; ++b)
+            for (int64_t k = p.off[i] / CF; k < p.off[i + 1] / CF; ++k) r.comp_active += tot[b * nchk + k];
+        r.comp_walked = walked;  // unit total
+    }
+    return MM_OK;
+}
+
+// A unit of a batch: one track, or consecutive same-settings tracks fused into one
+// timeline of at most MM_FUSE_MAX_FRAMES frames (default 72 M: a bigger timeline's
+// compacted envelope arrays span GBs per band, and their column-strided
+// scatters and walks miss the TLB: C5's 16 x 3-min 96 kHz as one unit ran its
+// compaction 3x slower per frame than as four).
+struct BatchUnit {
+    int first = 0, count = 1;
+    FusedPlan plan;
+};
+
+static std::vector<BatchUnit> batch_units(const mm_job *J, int n) {
+    int64_t cap = 72000000;
+    if (const char *e = getenv("MM_FUSE_MAX_FRAMES")) cap = std::max<int64_t>(0, atoll(e));
+    const bool fuse = !getenv("MM_BATCH_STREAMS_ONLY");
+    std::vector<BatchUnit> units;
+    for (int i = 0; i < n;) {
+        BatchUnit u;
+        u.first = i;
+        int k = 1;
+        if (fuse) {
+            const int64_t CF = (int64_t)J[i].tile * J[i].tiles_per_chunk;
+            int64_t frames = (J[i].frames_proc + CF - 1) / CF * CF;
+            while (i + k < n) {
+                const mm_job pair[2] = {J[i], J[i + k]};
+                const int64_t add = (J[i + k].frames_proc + CF - 1) / CF * CF;
+                if (!fusable(pair, 2) || frames + add > cap) break;
+                frames += add;
+                ++k;
+            }
+        }
+        u.count = k;
+        if (k > 1 && !fused_layout(J + i, k, &u.plan)) u.count = k = 1;
+        units.push_back(std::move(u));
+        i += k;
+    }
+    return units;
+}
+
 // =================================================================== C-ABI
 extern "C" {
 
@@ -897,17 +1196,21 @@ int mm_master_device(mm_ctx *c, const mm_job *j, const void *d_in, void *d_out, 
     return master_device(c, j, d_in, d_out, res);
 }
 
-// A batch of independent tracks (BASELINE C3/C5 on one GPU): job i runs on child
-// context i % S (own stream and buffers, S = min(n, MM_BATCH_STREAMS)), so the
-// chains of up to S tracks are in flight at once and their latency-bound kernels
-// fill each other's idle SIMDs.  Jobs are completed in submission order; a
-// child's next job is queued as soon as its previous one has been checked.
+// A batch of independent tracks (BASELINE C3/C5 on one GPU), cut into units
+// (batch_units: same-settings runs fused into one timeline, else single tracks);
+// unit u runs on child context u % S (own stream and buffers, S = min(units,
+// MM_BATCH_STREAMS)), so up to S units are in flight at once and their
+// latency-bound kernels fill each other's idle SIMDs.  Units are completed in
+// submission order; a child's next unit is queued as soon as its previous one
+// has been checked.
 int mm_master_batch(mm_ctx *c, int n, const mm_job *jobs, const void *const *d_in, void *const *d_out,
                     mm_result *res) {
     if (!c || n < 0 || (n > 0 && (!jobs || !d_in || !d_out))) return set_err(c, MM_ERR_ARG, "bad arguments");
     HIPCHK(c, hipSetDevice(c->device));
     for (int i = 0; i < n; ++i) RET(validate(c, &jobs[i]));
-    const int S = std::min(n, MM_BATCH_STREAMS);
+    std::vector<BatchUnit> units = batch_units(jobs, n);
+    const int nu = (int)units.size();
+    const int S = std::min(nu, MM_BATCH_STREAMS);
     while ((int)c->children.size() < S) {
         mm_ctx *k = nullptr;
         if (mm_create(c->device, &k) != MM_OK) return set_err(c, MM_ERR_HIP, "cannot create a batch stream");
@@ -917,6 +1220,16 @@ int mm_master_batch(mm_ctx *c, int n, const mm_job *jobs, const void *const *d_i
         c->children[s]->timing = c->timing;
         c->children[s]->concurrency = S;
     }
+    auto enqueue = [&](mm_ctx *k, BatchUnit &u) {
+        const int f = u.first;
+        if (u.count == 1) return enqueue_chain(k, &jobs[f], d_in[f], d_out[f]);
+        return fused_enqueue(k, u.count, jobs + f, d_in + f, d_out + f, u.plan);
+    };
+    auto complete = [&](mm_ctx *k, BatchUnit &u) {
+        const int f = u.first;
+        if (u.count == 1) return complete_chain(k, &jobs[f], d_out[f], res ? &res[f] : nullptr);
+        return fused_complete(k, u.count, jobs + f, d_out + f, res ? res + f : nullptr, u.plan);
+    };
     std::vector<int> cur((size_t)S, -1);
     int next = 0;
     auto fail = [&](mm_ctx *k) {
@@ -924,21 +1237,20 @@ int mm_master_batch(mm_ctx *c, int n, const mm_job *jobs, const void *const *d_i
         for (int s = 0; s < S; ++s) hipStreamSynchronize(c->children[s]->stream);
         return MM_ERR_STATE;
     };
-    for (int s = 0; s < S && next < n; ++s, ++next) {
+    for (int s = 0; s < S && next < nu; ++s, ++next) {
         cur[s] = next;
-        if (enqueue_chain(c->children[s], &jobs[next], d_in[next], d_out[next]) != MM_OK) return fail(c->children[s]);
+        if (enqueue(c->children[s], units[next]) != MM_OK) return fail(c->children[s]);
     }
-    for (int done = 0; done < n;) {
+    for (int done = 0; done < nu;) {
         for (int s = 0; s < S; ++s) {
             if (cur[s] < 0) continue;
             mm_ctx *k = c->children[s];
-            const int i = cur[s];
-            if (complete_chain(k, &jobs[i], d_out[i], res ? &res[i] : nullptr) != MM_OK) return fail(k);
+            if (complete(k, units[cur[s]]) != MM_OK) return fail(k);
             ++done;
             cur[s] = -1;
-            if (next < n) {
+            if (next < nu) {
                 cur[s] = next;
-                if (enqueue_chain(k, &jobs[next], d_in[next], d_out[next]) != MM_OK) return fail(k);
+                if (enqueue(k, units[next]) != MM_OK) return fail(k);
                 ++next;
             }
         }

@@ -211,8 +211,10 @@ def master_device(ctx: native.Context, job: Job, d_in: int, d_out: int, res: nat
 
 def master_batch(ctx: native.Context, jobs, d_ins, d_outs, with_results: bool = True):
     """A batch of independent tracks with device-resident inputs/outputs
-    (mm_master_batch): up to native.BATCH_STREAMS of them in flight at once, each on
-    its own stream.  Returns one MMResult per job (or None)."""
+    (mm_master_batch).  Tracks with the same settings run as ONE timeline (each on
+    whole chunks, every stage launched once for the batch); otherwise up to
+    native.BATCH_STREAMS of them are in flight at once, each on its own stream.
+    Returns one MMResult per job (or None)."""
     n = len(jobs)
     arr = (native.MMJob * n)(*[j.job for j in jobs])
     ins = (ctypes.c_void_p * n)(*[ctypes.c_void_p(int(p)) for p in d_ins])

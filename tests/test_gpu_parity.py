@@ -184,3 +184,42 @@ def test_compressor_resume_path(oracle, monkeypatch, warmup):
     assert info["comp_iters"] >= 1, info["comp_iters"]  # the one queued sweep changed ends
     ref, L = oracle.master(pcm, 44100, P_HOT, return_loudness=True)
     _check(out, info, ref, L)
+
+
+@pytest.mark.parametrize("channels,params,in_i16", [(2, P_FULL, False), (1, P_HOT, True),
+                                                     (2, dict(P_FULL, lufs=None), False)],
+                         ids=["stereo_full", "mono_hot_i16", "stereo_nolufs"])
+def test_fused_batch_ragged(oracle, monkeypatch, channels, params, in_i16):
+    """mm_master_batch fuses same-settings tracks into one timeline (whole chunks
+    per track, the last one zero-padded): ragged lengths (sub-chunk, chunk + a
+    fraction, exactly one chunk, a sub-second clip) each against the oracle, and
+    the stream path (MM_BATCH_STREAMS_ONLY) gives the same loudness."""
+    import torch
+
+    from mastering_amd import Job, master_batch, native
+    from mastering_amd.synth import pink_noise_pcm16
+    rate = 44100
+    lens = [int(3.2 * rate), int(31.7 * rate), 30 * rate, int(0.7 * rate), int(62.05 * rate)]
+    pcms = [pink_noise_pcm16(n, rate, channels, 900 + t) for t, n in enumerate(lens)]
+    kind = native.MM_IN_I16 if in_i16 else native.MM_IN_F32
+    xs = [torch.from_numpy(p.copy() if in_i16 else p.astype(np.float32) / 32768).cuda() for p in pcms]
+    jobs = [Job(n, rate, channels, params) for n in lens]
+    for j in jobs:
+        j.job.in_kind = kind
+    ctx = native.context(0)
+
+    def run():
+        outs = [torch.full((j.frames_proc, channels), 12345, dtype=torch.int16, device="cuda") for j in jobs]
+        res = master_batch(ctx, jobs, [x.data_ptr() for x in xs], [o.data_ptr() for o in outs])
+        return [o.cpu().numpy() for o in outs], res
+
+    outs, res = run()
+    for t, pcm in enumerate(pcms):
+        ref, L = oracle.master(pcm, rate, params, return_loudness=True)
+        _check(outs[t].reshape(ref.shape), {"loudness": res[t].loudness}, ref, L)
+    monkeypatch.setenv("MM_BATCH_STREAMS_ONLY", "1")
+    outs2, res2 = run()
+    for t in range(len(pcms)):
+        if params.get("lufs") is not None:
+            assert abs(res[t].loudness - res2[t].loudness) <= 1e-9
+        assert rms_diff(outs[t], outs2[t]) <= RMS_TOL and np.mean(outs[t] == outs2[t]) >= 0.9999
