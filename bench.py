@@ -6,9 +6,9 @@ the rank's share once, inputs and outputs resident in HBM):
       config).  With N > 1 every rank masters its own track: file sharding, no
       data-path collective, "scaling": "weak".
   C3  8 x 3-min 44.1 kHz tracks per GPU (64 tracks over 8 GPUs), file-sharded,
-      run as one mm_master_batch: same-settings tracks fused into one timeline
-      (units of <= 72 M frames, every stage launched once per unit), units in
-      flight on their own streams.
+      run as one mm_master_batch: same-settings tracks fused into timelines
+      (two units here, every stage launched once per unit), units in flight on
+      their own streams.
   C4  one 2-h 44.1 kHz track time-sharded over the N ranks: each rank stages its
       contiguous 30 s chunks, then the K-weighting carry all-gather and ONE sum
       all-reduce of the 0.1 s loudness energies run through the library's own RCCL

@@ -1101,39 +1101,60 @@ static int fused_complete(mm_ctx *c, int n, const mm_job *J, void *const *d_out,
 }
 
 // A unit of a batch: one track, or consecutive same-settings tracks fused into one
-// timeline of at most MM_FUSE_MAX_FRAMES frames (default 72 M: a bigger timeline's
-// compacted envelope arrays span GBs per band, and their column-strided
-// scatters and walks miss the TLB: C5's 16 x 3-min 96 kHz as one unit ran its
-// compaction 3x slower per frame than as four).
+// timeline.  A run of such tracks is split into max(2, ceil(frames / cap)) units of
+// about equal length (cap MM_FUSE_MAX_FRAMES, default 150 M frames): two units in
+// flight on two streams overlap one unit's latency-bound tail with the other's
+// front (C3 8 x 3 min: 14.5 G frames/s as 2 units, 14.2 as 1, 13.7 as 4; C5 16 x 3
+// min at 96 kHz: 12.6 as 2, 12.3 as 4, 12.0 as 1, 11.0 unfused), and the cap
+// keeps a unit's compacted envelope arrays to a few GB.
 struct BatchUnit {
     int first = 0, count = 1;
     FusedPlan plan;
 };
 
 static std::vector<BatchUnit> batch_units(const mm_job *J, int n) {
-    int64_t cap = 72000000;
-    if (const char *e = getenv("MM_FUSE_MAX_FRAMES")) cap = std::max<int64_t>(0, atoll(e));
+    int64_t cap = 150000000;
+    if (const char *e = getenv("MM_FUSE_MAX_FRAMES")) cap = std::max<int64_t>(1, atoll(e));
     const bool fuse = !getenv("MM_BATCH_STREAMS_ONLY");
+    auto padded = [&](int i) {
+        const int64_t CF = (int64_t)J[i].tile * J[i].tiles_per_chunk;
+        return (J[i].frames_proc + CF - 1) / CF * CF;
+    };
     std::vector<BatchUnit> units;
     for (int i = 0; i < n;) {
-        BatchUnit u;
-        u.first = i;
-        int k = 1;
-        if (fuse) {
-            const int64_t CF = (int64_t)J[i].tile * J[i].tiles_per_chunk;
-            int64_t frames = (J[i].frames_proc + CF - 1) / CF * CF;
-            while (i + k < n) {
-                const mm_job pair[2] = {J[i], J[i + k]};
-                const int64_t add = (J[i + k].frames_proc + CF - 1) / CF * CF;
-                if (!fusable(pair, 2) || frames + add > cap) break;
-                frames += add;
-                ++k;
-            }
+        int run = 1;  // maximal run of tracks fusable with track i
+        int64_t total = padded(i);
+        while (fuse && i + run < n) {
+            const mm_job pair[2] = {J[i], J[i + run]};
+            if (!fusable(pair, 2)) break;
+            total += padded(i + run);
+            ++run;
         }
-        u.count = k;
-        if (k > 1 && !fused_layout(J + i, k, &u.plan)) u.count = k = 1;
-        units.push_back(std::move(u));
-        i += k;
+        const int parts = (int)std::min<int64_t>(run, std::max<int64_t>(std::min(2, run), (total + cap - 1) / cap));
+        int64_t acc = 0;
+        int k = i;
+        for (int q = 0; q < parts; ++q) {  // close unit q once it holds about (q+1)/parts of the run
+            BatchUnit u;
+            u.first = k;
+            if (q + 1 == parts) {
+                k = i + run;
+            } else {
+                const int64_t goal = total * (q + 1) / parts;
+                acc += padded(k++);
+                while (k < i + run - (parts - q - 1) && acc + padded(k) / 2 <= goal) acc += padded(k++);
+            }
+            u.count = k - u.first;
+            if (u.count > 1 && !fused_layout(J + u.first, u.count, &u.plan)) {  // over 2^31 frames: one by one
+                for (int t = u.first; t < k; ++t) {
+                    BatchUnit v;
+                    v.first = t;
+                    units.push_back(std::move(v));
+                }
+                continue;
+            }
+            units.push_back(std::move(u));
+        }
+        i += run;
     }
     return units;
 }
