@@ -58,6 +58,9 @@ __device__ __forceinline__ uint32_t rms_exact(double S, double n, float inv_n) {
     return n > 0.0 ? (uint32_t)r : 0u;
 }
 
+#ifndef MM_RMS_NB
+#define MM_RMS_NB 3
+#endif
 // 1. rms per frame (uint16 r, tile-major).  grid: (ceil(G/256), 3 bands).  The
 // window [max(chunk0, f-look), f) slides one frame per step: + frame f-1 (this
 // lane's own previous frame), - frame f-1-look (up to ~4 tiles back: another
@@ -99,7 +102,7 @@ __global__ void __launch_bounds__(256) comp_rms_kernel(CompArgs a) {
     struct Pair {
         short2 in, drop;
     };
-    stream<8, 3, Pair>(
+    stream<8, MM_RMS_NB, Pair>(
         len,
         [&](int i) {
             i = min(i, len - 1);

@@ -59,6 +59,12 @@ __device__ __forceinline__ double df2t(double x, double &z0, double &z1, const d
 #ifndef MM_XO_NB
 #define MM_XO_NB 3
 #endif
+#ifndef MM_EQ_NB
+#define MM_EQ_NB 3
+#endif
+#ifndef MM_KW_NB
+#define MM_KW_NB 3
+#endif
 constexpr int EQ_STAGE = MM_EQ_STAGE;  // frames per tile staged through LDS per step
 
 struct EqArgs {
@@ -181,7 +187,7 @@ __device__ void eq_pass2(const EqArgs &a, int64_t g, int c, int len, double (&z)
     const int64_t G = a.G;
     const float *xs = a.xs;
     int n = 0;
-    stream<8, 3, float>(
+    stream<8, MM_EQ_NB, float>(
         len, [&](int i) { return xs[((int64_t)min(i, len - 1) * G + g) * CH + c]; },
         [&](float x) {
             double y = (double)x;
@@ -415,7 +421,7 @@ __device__ __forceinline__ void kw_pass(const KwArgs &a, int64_t g, int len, dou
     const short2 *mix = reinterpret_cast<const short2 *>(a.mix) + (g - gt * a.sub) * a.T * a.Gt + gt;
     const int64_t Gt = a.Gt;
     int64_t pf = g * a.T;
-    stream<8, 3, short2>(
+    stream<8, MM_KW_NB, short2>(
         len, [&](int i) { return mix[(int64_t)min(i, len - 1) * Gt]; },
         [&](short2 q) {
             const float m = a.ch == 2 ? ((float)q.x + (float)q.y) * (1.0f / 65536.0f)

@@ -64,6 +64,7 @@ struct mm_ctx {
     uint32_t *ctl_claims = nullptr;     // its zeroed claim stamps
     int comp_iters = 0, comp_pending = 0;
     int comp_hint = 0;  // sweeps the last converged solve of this context needed, + 1 (0: none yet)
+    int warm_extra = 0;  // adaptive warm-up: super-tiles added to the job's (evaluate_chain)
     unsigned comp_nb = 0;
     // loudness on the device
     double *gate_out = nullptr;         // [2]: L, gain
@@ -303,6 +304,8 @@ static int launch_eq(mm_ctx *c, int nsec, int ch, unsigned nblk, const EqArgs &e
 // Convergence is checked at the chain's single sync (evaluate_chain); a rare
 // unconverged batch is extended there (MM_COMP_SWEEPS sets the queued count).
 constexpr int COMP_SWEEPS = 6;  // queued by a context's first chain; later ones follow comp_hint
+constexpr int WARM_EXTRA = 6;   // adaptive warm-up step (super-tiles)
+constexpr int WARM_ADAPT_MIN = 4;  // jobs with a shorter warm-up (tests of the resume path) are left as set
 
 static int comp_sweeps(mm_ctx *c, int n) {
     CompArgs &ca = c->ca;
@@ -368,7 +371,21 @@ static int evaluate_chain(mm_ctx *c, bool *converged) {
         c->comp_iters += k;
         *converged = k < c->comp_pending;
         c->comp_pending = 0;
-        if (*converged) c->comp_hint = std::max(2, std::min(16, c->comp_iters + 2));
+        if (*converged) {
+            c->comp_hint = std::max(2, std::min(16, c->comp_iters + 2));
+            // Adaptive warm-up (jobs at the default warm-up or more): heavily
+            // compressed material coalesces late, so a solve that
+            // re-walked over 1 % of its active frames raises the next solve's
+            // warm-up by WARM_EXTRA super-tiles, and one that re-walked under
+            // 0.02 % drops it again (C2 at P_HOT: 2.52 -> 2.01 ms; P_FULL keeps 6,
+            // where 9 costs 6 %).
+            int64_t active = 0;
+            const int32_t *tot = reinterpret_cast<const int32_t *>(c->rb + RB_TOTALS);
+            for (int64_t k = 0; k < 3 * comp_chunks(c); ++k) active += tot[k];
+            const double walked = (double)*reinterpret_cast<const unsigned long long *>(c->rb + RB_WALKED);
+            if (walked > 0.01 * (double)active) c->warm_extra = WARM_EXTRA;
+            else if (walked < 2e-4 * (double)active) c->warm_extra = 0;
+        }
         if (!*converged && c->comp_iters >= c->job.comp_max_iters)
             return set_err(c, MM_ERR_STATE, "compressor did not converge in %d sweeps", c->comp_iters);
     }
@@ -432,7 +449,7 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     ca.T = T;
     ca.K = K;
     ca.ch = ch;
-    ca.warmup = j->comp_warmup;
+    ca.warmup = j->comp_warmup + (j->comp_warmup >= WARM_ADAPT_MIN ? c->warm_extra : 0);
     int64_t nchunks;
     comp_geometry(j, G, &ca.U, &ca.SPC, &nchunks);
     ca.GS = nchunks * ca.SPC;
