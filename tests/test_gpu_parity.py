@@ -223,3 +223,25 @@ def test_fused_batch_ragged(oracle, monkeypatch, channels, params, in_i16):
         if params.get("lufs") is not None:
             assert abs(res[t].loudness - res2[t].loudness) <= 1e-9
         assert rms_diff(outs[t], outs2[t]) <= RMS_TOL and np.mean(outs[t] == outs2[t]) >= 0.9999
+
+
+def test_batch_mixed_settings_units(oracle):
+    """A batch whose settings change along it: same-settings runs become fused units
+    (split in two), a lone track stays a single chain, and every result lands in its
+    own slot (each track against the oracle with its own settings)."""
+    import torch
+
+    from mastering_amd import Job, master_batch, native
+    from mastering_amd.synth import pink_noise_pcm16
+    rate = 44100
+    plan = [(P_FULL, 4.1), (P_FULL, 31.0), (P_FULL, 2.2), (P_HOT, 3.3), (P_HOT, 5.0), (P_FULL, 1.5),
+            (dict(P_FULL, lufs=None), 2.0)]
+    pcms = [pink_noise_pcm16(int(s * rate), rate, 2, 700 + t) for t, (_, s) in enumerate(plan)]
+    jobs = [Job(p.shape[0], rate, 2, st) for p, (st, _) in zip(pcms, plan)]
+    xs = [torch.from_numpy(p.astype(np.float32) / 32768).cuda() for p in pcms]
+    outs = [torch.empty((j.frames_proc, 2), dtype=torch.int16, device="cuda") for j in jobs]
+    res = master_batch(native.context(0), jobs, [x.data_ptr() for x in xs], [o.data_ptr() for o in outs])
+    for t, (pcm, (st, _)) in enumerate(zip(pcms, plan)):
+        ref, L = oracle.master(pcm, rate, st, return_loudness=True)
+        assert res[t].frames_out == jobs[t].frames_proc
+        _check(outs[t].cpu().numpy(), {"loudness": res[t].loudness}, ref, L)
