@@ -186,10 +186,11 @@ def test_compressor_resume_path(oracle, monkeypatch, warmup):
     _check(out, info, ref, L)
 
 
-@pytest.mark.parametrize("channels,params,in_i16", [(2, P_FULL, False), (1, P_HOT, True),
-                                                     (2, dict(P_FULL, lufs=None), False)],
-                         ids=["stereo_full", "mono_hot_i16", "stereo_nolufs"])
-def test_fused_batch_ragged(oracle, monkeypatch, channels, params, in_i16):
+@pytest.mark.parametrize("channels,params,in_i16,rate", [(2, P_FULL, False, 44100), (1, P_HOT, True, 44100),
+                                                          (2, dict(P_FULL, lufs=None), False, 44100),
+                                                          (2, P_HOT, True, 48000)],
+                         ids=["stereo_full", "mono_hot_i16", "stereo_nolufs", "stereo_hot_48k"])
+def test_fused_batch_ragged(oracle, monkeypatch, channels, params, in_i16, rate):
     """mm_master_batch fuses same-settings tracks into one timeline (whole chunks
     per track, the last one zero-padded): ragged lengths (sub-chunk, chunk + a
     fraction, exactly one chunk, a sub-second clip) each against the oracle, and
@@ -198,7 +199,6 @@ def test_fused_batch_ragged(oracle, monkeypatch, channels, params, in_i16):
 
     from mastering_amd import Job, master_batch, native
     from mastering_amd.synth import pink_noise_pcm16
-    rate = 44100
     lens = [int(3.2 * rate), int(31.7 * rate), 30 * rate, int(0.7 * rate), int(62.05 * rate)]
     pcms = [pink_noise_pcm16(n, rate, channels, 900 + t) for t, n in enumerate(lens)]
     kind = native.MM_IN_I16 if in_i16 else native.MM_IN_F32
