@@ -125,7 +125,18 @@ def parse():
     ap.add_argument("--cpu-procs", type=int, default=0, help="worker processes of the N-core leg (0: the box's "
                                                               "cores, at most 16)")
     ap.add_argument("--profile-tag", default=None, help="profiles/<tag>_pmc_summary.json for traffic/limiter")
-    return ap.parse_args()
+    ap.add_argument("--tune", action="append", default=[], metavar="NAME=INT",
+                    help="tuning experiments only: set engine.NAME (COMP_WARMUP, COMP_SUPER_FRAMES) or "
+                         "design.DEFAULT_TILE before the jobs are planned")
+    args = ap.parse_args()
+    for kv in args.tune:
+        name, val = kv.split("=")
+        from mastering_amd import design, engine
+        mod = design if name == "DEFAULT_TILE" else engine
+        if not hasattr(mod, name):
+            raise SystemExit(f"--tune: unknown knob {name}")
+        setattr(mod, name, int(val))
+    return args
 
 
 # ----------------------------------------------------------------- CPU baseline
@@ -315,6 +326,8 @@ def main():
             else 0
         walked = sum(int(getattr(r, "comp_walked", 0) or 0) for r in res) if res and not isinstance(res[0], dict) \
             else 0
+        jumped = sum(int(getattr(r, "comp_jumped", 0) or 0) for r in res) if res and not isinstance(res[0], dict) \
+            else 0
         iters = [int(r.comp_iters) for r in res] if res and not isinstance(res[0], dict) else None
         job0 = run.jobs[0]
         n_frames = run.frames_step
@@ -362,7 +375,7 @@ def main():
                                              "algorithmic_bytes_per_launch": bpl, "avg_launch_ms": avg_s * 1e3,
                                              "launches_per_step": launches, "traffic": dom_traffic}},
             "chain": {"device_ms_per_step": sum(v[0] for v in per.values()),
-                      "comp_iters": iters, "comp_active_frames": active, "comp_rewalked_frames": walked,
+                      "comp_iters": iters, "comp_active_frames": active, "comp_rewalked_frames": walked, "comp_jumped_frames": jumped,
                       "kernels_ms_per_step": {k: round(v[0], 4) for k, v in per.items()}},
         }
         if args.workload == "C4":

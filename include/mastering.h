@@ -77,9 +77,11 @@ typedef struct mm_band {
     const double *lut;       /* host table [32769][4] per integer rms r:
                                 {M, M/attack_frames, M/release_frames, 0} with
                                 M = (1-1/ratio)*max(20*log(r/thr,10), 0) (0 if r
-                                == 0), all in Python float arithmetic.  Immutable
-                                while the context holds it (uploaded once per
-                                distinct pointer)                              */
+                                == 0), all in Python float arithmetic          */
+    uint64_t lut_key;        /* content key of the M column of lut (nonzero; the
+                                context uploads a table only when the key of its
+                                cached copy differs).  0: no key, uploaded on
+                                every call                                     */
 } mm_band;
 
 /* A mastering job for one track (geometry + settings, all host memory). */
@@ -126,6 +128,7 @@ typedef struct mm_result {
     int32_t _pad;
     int64_t comp_active;     /* active (M != 0) frames over the three bands      */
     int64_t comp_walked;     /* frames re-walked by the fix-up sweeps            */
+    int64_t comp_jumped;     /* frames the sweeps crossed by exact release jumps */
 } mm_result;
 
 /* ---- context ------------------------------------------------------------ */

@@ -160,9 +160,19 @@ struct CompArgs {
     double *start[3];          // per-super-tile start state
     double *end[3];            // per-super-tile end state (one buffer; sweeps hand ends over with sc1 accesses)
     uint32_t *claim[3];        // per super-tile: the last sweep stamp that claimed it (zeroed per chain)
+    int SPT;                   // jump segments per super-tile (U / SEG)
+    double *desc[3];           // release-jump descriptors [GS][SPT][2 + 2 JB] (compressor.hip SegDesc)
+    double *jstart[3];         // per segment: entry state recorded by the sweep that jumped it
+    uint32_t *jmark[3];        // per segment: chain tag of that jump (0 / older tags: none this chain)
+    uint32_t tag;              // this chain's tag (never 0)
+    uint32_t *jlist[3];        // per band: segments (t * GS + s) newly marked this chain, for comp_refill
+    uint32_t *jlist_n;         // [3] their counts (zeroed per chain; > jlist_cap: overflowed, refill scans all)
+    uint32_t jlist_cap;
+    int jumps;                 // release jumps enabled (MM_COMP_NOJUMP=1 disables them: diagnostics)
     uint32_t stamp;            // this sweep's stamp (> every earlier one of the chain)
+    int heads;                 // 0: Jacobi sweep (every stale super-tile walks); 1: run heads only
     unsigned int *changed;
-    unsigned long long *walked;  // frames re-walked by the fix-up sweeps (statistics)
+    unsigned long long *walked;  // [0] frames re-walked, [1] frames jumped by the fix-up sweeps (statistics)
     short2 *q_out;
 };
 

@@ -267,6 +267,9 @@ __device__ __forceinline__ BandStep band_step(const CompArgs &a, int b) {
     return s;
 }
 
+// IEEE binade of a positive normal double: x in [2^e, 2^(e+1))
+__device__ __forceinline__ int binade(double x) { return (int)((uint64_t)__double_as_longlong(x) >> 52) - 1023; }
+
 // One envelope step, exactly pydub's
 //   if rms > thr and att <= M: att = min(att + M/A, M)
 //   else:                      att = max(att - M/R, 0)
@@ -325,9 +328,18 @@ __device__ __forceinline__ double lean_step(double att, double m, double inc, do
 // uses them, so they issue while the att chain of earlier frames is in flight
 // (in-order issue: tools/micro/walk2_bench.hip, 136 -> 98 cycles per step).
 // With CK (an owning walk), store the state on entry to every CK_Q-th frame.
-constexpr int WALK_WB = 32;  // M values in flight per walker
+#ifndef MM_WALK_WB
+#define MM_WALK_WB 40
+#endif
+constexpr int WALK_WB = MM_WALK_WB;  // M values in flight per walker (a multiple of CK_Q)
 constexpr int WALK_PAD = WALK_WB;  // padding rows after the compacted array (prefetch past a super-tile's end)
-constexpr int CK_Q = 8;      // checkpoint stride (compacted frames); divides WALK_WB and U
+constexpr int CK_Q = 10;     // checkpoint stride (compacted frames); divides WALK_WB and SEG
+// Release jumps: a super-tile is cut into segments of SEG compacted
+// frames; for each, pass 0 records the exact effect of SEG release steps on any
+// state of binade e0 + k (k < JB, per mantissa parity), so a fix-up walker whose
+// exact state releases through the whole segment moves past it in O(1).
+constexpr int SEG = 100;     // divides U (host), multiple of CK_Q and DESC_B
+constexpr int JB = 4;        // binades per segment descriptor: e0 .. e0 + JB - 1
 
 // A column of Mc / ck walked row by row.  BUF: buffer loads/stores with the
 // column's byte offset in a VGPR (constant over the walk) and the row's in an
@@ -339,8 +351,10 @@ template <>
 struct ColWalk<false> {
     double *p;
     size_t step;
-    __device__ __forceinline__ ColWalk(const double *base, int64_t col, int64_t rs, uint32_t)
-        : p(const_cast<double *>(base) + col), step((size_t)rs) {}
+    // rows rs elements apart from row row0 (or from element offset `skip` when given)
+    __device__ __forceinline__ ColWalk(const double *base, int64_t col, int64_t rs, uint32_t, int row0 = 0,
+                                       int64_t skip = -1)
+        : p(const_cast<double *>(base) + col + (skip >= 0 ? skip : (int64_t)row0 * rs)), step((size_t)rs) {}
     __device__ __forceinline__ double ld() {
         const double v = *p;
         p += step;
@@ -353,31 +367,36 @@ struct ColWalk<false> {
 };
 template <>
 struct ColWalk<true> {
+    // the row offset advances in the per-lane (VGPR) offset: lanes walk different
+    // rows and trip counts (an SGPR offset that diverges becomes a waterfall loop
+    // around every load); the SGPR offset stays 0
     __amdgpu_buffer_rsrc_t r;
-    int vo, so, step;
-    __device__ __forceinline__ ColWalk(const double *base, int64_t col, int64_t rs, uint32_t bytes)
+    int vo, step;
+    __device__ __forceinline__ ColWalk(const double *base, int64_t col, int64_t rs, uint32_t bytes, int row0 = 0,
+                                       int64_t skip = -1)
         : r(__builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(base), (short)0, (int)bytes, 0x00020000)),
-          vo((int)(col * 8)), so(0), step((int)(rs * 8)) {}
+          vo((int)((col + (skip >= 0 ? skip : (int64_t)row0 * rs)) * 8)), step((int)(rs * 8)) {}
     __device__ __forceinline__ double ld() {
-        const double v = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0));
-        so += step;
+        const double v = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vo, 0, 0));
+        vo += step;
         return v;
     }
     __device__ __forceinline__ void st(double v) {
         typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, vo, so, 0);
-        so += step;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, vo, 0, 0);
+        vo += step;
     }
 };
 
 template <bool CK, bool BUF = false>
 __device__ __forceinline__ double comp_walk(double att, const CompArgs &a, int b, int64_t s, int len,
-                                            const BandStep &bs) {
+                                            const BandStep &bs, int row0 = 0) {
     constexpr int WB = WALK_WB, WP = 4;
     if (len <= 0) return att;
-    // column s, rows RS apart; loads run up to WB rows past the end (padding rows)
-    ColWalk<BUF> pl(a.Mc[b], cm_col(a, s), a.RS, a.mc_bytes);
-    ColWalk<BUF> pc(CK ? a.ck[b] : a.Mc[b], CK ? ck_col(a, s) : 0, a.RS, a.ck_bytes);  // checkpoint rows
+    // column s from row row0 (a multiple of CK_Q), rows RS apart; loads run up to WB
+    // rows past the end (padding rows)
+    ColWalk<BUF> pl(a.Mc[b], cm_col(a, s), a.RS, a.mc_bytes, row0);
+    ColWalk<BUF> pc(CK ? a.ck[b] : a.Mc[b], CK ? ck_col(a, s) : 0, a.RS, a.ck_bytes, CK ? row0 / CK_Q : 0);  // checkpoint rows
     double buf[WB], inc[WP], dec[WP];
 #pragma unroll
     for (int k = 0; k < WB; ++k) buf[k] = pl.ld();
@@ -414,23 +433,24 @@ __device__ __forceinline__ double comp_walk(double att, const CompArgs &a, int b
     return att;
 }
 
-// Re-walk of a super-tile by a fix sweep: comp_walk<true> from the corrected
-// start, which also compares the state at every WB-frame block start with the
-// checkpoint stored there by the previous walk (loaded one block ahead, before
-// this walk overwrites it).  Equal states mean the stored trajectory from there
-// on (and the stored end) came from the same state: the walk stops (coalesced).
-// Returns the end state (meaningless when coalesced); *nw = frames walked.
+// Re-walk of segment [i0, i0 + sl) of a super-tile by a fix sweep: comp_walk<true>
+// from the corrected state, which also compares the state at every WB-frame
+// block start with the checkpoint stored there by the previous walk (loaded one
+// block ahead, before this walk overwrites it).  Equal states mean the stored
+// trajectory from there on (and the stored end) came from the same state: the
+// walk stops (coalesced).  Returns the state after the segment (meaningless when
+// coalesced); *nw = frames walked.
 template <bool BUF>
-__device__ __forceinline__ double comp_rewalk(double att, const CompArgs &a, int b, int64_t s, int len,
-                                              const BandStep &bs, bool *coalesced, int *nw) {
+__device__ __forceinline__ double comp_rewalk_seg(double att, const CompArgs &a, int b, int64_t s, int i0, int sl,
+                                                  const BandStep &bs, bool *coalesced, int *nw, bool check = true) {
     constexpr int WB = WALK_WB, WP = 4, CKB = WB / CK_Q;  // checkpoint rows per block
     *coalesced = false;
-    *nw = len;
-    if (len <= 0) return att;
+    *nw = sl;
+    if (sl <= 0) return att;
     const int64_t cs = ck_col(a, s);
-    ColWalk<BUF> pl(a.Mc[b], cm_col(a, s), a.RS, a.mc_bytes);
-    ColWalk<BUF> pc(a.ck[b], cs, a.RS, a.ck_bytes);
-    ColWalk<BUF> po(a.ck[b], cs, CKB * a.RS, a.ck_bytes);  // old checkpoint of the next block start (padding rows)
+    ColWalk<BUF> pl(a.Mc[b], cm_col(a, s), a.RS, a.mc_bytes, i0);
+    ColWalk<BUF> pc(a.ck[b], cs, a.RS, a.ck_bytes, i0 / CK_Q);
+    ColWalk<BUF> po(a.ck[b], cs, CKB * a.RS, a.ck_bytes, 0, (int64_t)(i0 / CK_Q) * a.RS);  // old checkpoint of the next block start (padding rows)
     double buf[WB], inc[WP], dec[WP];
 #pragma unroll
     for (int k = 0; k < WB; ++k) buf[k] = pl.ld();
@@ -439,15 +459,18 @@ __device__ __forceinline__ double comp_rewalk(double att, const CompArgs &a, int
         inc[k] = div_cr(buf[k], bs.A, bs.rA);
         dec[k] = div_cr(buf[k], bs.R, bs.rR);
     }
-    double old = po.ld();
+    // (with !check the stored checkpoints inside the segment are not this
+    // trajectory's: never compared; NaN never equals a state)
+    const double nan = __longlong_as_double(0x7ff8000000000000ll);
+    double old = check ? po.ld() : nan;
     int i = 0;
-    for (; i + WB <= len; i += WB) {
+    for (; i + WB <= sl; i += WB) {
         if (__double_as_longlong(old) == __double_as_longlong(att)) {
             *coalesced = true;
             *nw = i;
             return att;
         }
-        old = po.ld();
+        old = check ? po.ld() : nan;
 #pragma unroll
         for (int k = 0; k < WB; ++k) {
             const double m = buf[k], ik = inc[k % WP], dk = dec[k % WP];
@@ -459,7 +482,7 @@ __device__ __forceinline__ double comp_rewalk(double att, const CompArgs &a, int
             buf[k] = pl.ld();
         }
     }
-    const int rem = len - i;
+    const int rem = sl - i;
     if (rem > 0 && __double_as_longlong(old) == __double_as_longlong(att)) {
         *coalesced = true;
         *nw = i;
@@ -479,14 +502,189 @@ __device__ __forceinline__ double comp_rewalk(double att, const CompArgs &a, int
     return att;
 }
 
-// 4. speculative pass.  grid: (ceil(GS/(own*BLOCK)), 3).  Each lane walks `own`
-// consecutive super-tiles.  The start of the first is guessed by walking the
-// `warmup` previous super-tiles of its chunk, from the M of the first warm-up
-// frame (the state tracks M closely: this coalesces with the true trajectory far
-// more often than a start at 0; tools/ studies); the later ones start from the
-// end of the one before (a longer warm-up for free).  own > 1 divides the
-// warm-up walks (and their M re-reads) by own; the host raises it with the
-// problem size (more super-tiles than the chip needs lanes).
+// ---- release jumps -----------------------------------------------------------
+// Exactness ("release jumps").  Let a be a double in binade e
+// (2^e <= a < 2^(e+1)), so a = A u with u = 2^(e-52) and integer A.  A release step
+// a' = RN(a - d) whose exact result a - d stays >= 2^e rounds on the grid u:
+// a' = a - rho u with rho the nearest integer to d/u, a tie going to the even
+// result.  rho therefore depends only on d, e and the parity of A.  A reference
+// walk r that starts in binade e with the same parity and stays in it rounds
+// every step exactly like a, so after SEG release steps a ends at a - (r0 - rL).
+// Pass 0 walks 2 * JB such references per segment (binades e0 .. e0+JB-1, both
+// parities; e0 = binade of the segment's first M) and stores q = r0 - rL (exact,
+// NaN if the reference left its binade) and the segment's max M.  A fix-up walker
+// in state a (binade e, parity p) may jump iff x = a - q[e - e0][p] satisfies
+//   x > max M  (every entry state of the segment, all >= x, is > its M: release)
+//   x >= 2^e + u (every exact difference a_k - d_k >= a_{k+1} - u/2 > 2^e: grid u)
+// and then lands EXACTLY on the state the step-by-step walk reaches.
+struct SegDesc {
+    double mx;
+    int e0;
+    double q[2 * JB];
+};
+constexpr int DREC = 2 + 2 * JB;  // doubles per descriptor record: max M, e0, q[2 JB]
+
+// Record of segment t of super-tile s: [s][SPT][DREC] (a lane's records contiguous)
+__device__ __forceinline__ const double2 *desc_rec(const CompArgs &a, int b, int64_t s, int t) {
+    return reinterpret_cast<const double2 *>(a.desc[b] + ((s * a.SPT + t) * DREC));
+}
+__device__ __forceinline__ SegDesc load_desc(const double2 *r) {
+    SegDesc d;
+    double2 v[DREC / 2];
+#pragma unroll
+    for (int k = 0; k < DREC / 2; ++k) v[k] = r[k];
+    d.mx = v[0].x;
+    d.e0 = (int)v[0].y;
+#pragma unroll
+    for (int k = 0; k < JB; ++k) {
+        d.q[2 * k] = v[k + 1].x;
+        d.q[2 * k + 1] = v[k + 1].y;
+    }
+    return d;
+}
+
+__device__ __forceinline__ bool release_jump(const SegDesc &d, double att, double *out) {
+    constexpr uint64_t MANT = (1ull << 52) - 1;
+    const uint64_t ab = (uint64_t)__double_as_longlong(att);
+    const int k = (int)(ab >> 52) - 1023 - d.e0;
+    if (!(att > 0.0) || k < 0 || k >= JB) return false;
+    const int idx = 2 * k + (int)(ab & 1);
+    double q = d.q[0];
+#pragma unroll
+    for (int j = 1; j < 2 * JB; ++j) q = idx == j ? d.q[j] : q;
+    const double x = att - q;  // exact: both multiples of u, result checked to stay in binade e
+    const uint64_t xb = (uint64_t)__double_as_longlong(x);
+    if (!(x > d.mx) || (xb >> 52) != (ab >> 52) || (xb & MANT) == 0) return false;
+    *out = x;
+    return true;
+}
+
+// Descriptors of the full segments of super-tile s (pass 0's second wave): one
+// pass over the column, the 2 * JB reference walks per frame off any dependency
+// chain but their own.
+constexpr int DESC_B = 20;  // M values in flight per describing lane (divides SEG)
+
+__device__ __forceinline__ void comp_describe(const CompArgs &a, int b, int64_t s, int len, const BandStep &bs) {
+    constexpr int WB = DESC_B;
+    constexpr uint64_t MANT = (1ull << 52) - 1;
+    const int nseg = min(len / SEG, a.SPT);
+    if (nseg <= 0) return;
+    ColWalk<false> pl(a.Mc[b], cm_col(a, s), a.RS, 0);
+    double buf[WB];
+#pragma unroll
+    for (int k = 0; k < WB; ++k) buf[k] = pl.ld();
+    for (int t = 0; t < nseg; ++t) {
+        const int e0 = binade(buf[0]);  // buf[0] = the segment's first M (> 0)
+        double r0[2 * JB], r[2 * JB];
+#pragma unroll
+        for (int k = 0; k < 2 * JB; ++k) {  // top of binade e0 + k/2, parity k % 2
+            const uint64_t bits = ((uint64_t)(e0 + k / 2 + 1023) << 52) | (MANT - 63 + (uint64_t)(k % 2));
+            r0[k] = r[k] = __longlong_as_double((long long)bits);
+        }
+        double mx = 0.0;
+        for (int blk = 0; blk < SEG / WB; ++blk) {
+#pragma unroll
+            for (int k = 0; k < WB; ++k) {
+                const double m = buf[k];
+                const double dec = div_cr(m, bs.R, bs.rR);
+                mx = fmax(mx, m);
+#pragma unroll
+                for (int j = 0; j < 2 * JB; ++j) r[j] = r[j] - dec;
+                buf[k] = pl.ld();
+            }
+        }
+        double q[2 * JB];
+#pragma unroll
+        for (int k = 0; k < 2 * JB; ++k) {
+            // the reference stayed in its binade with a nonzero mantissa (>= 2^e + u) at the end
+            const uint64_t rb = (uint64_t)__double_as_longlong(r[k]);
+            const bool ok = (rb >> 52) == (uint64_t)(e0 + k / 2 + 1023) && (rb & MANT) != 0;
+            q[k] = ok ? r0[k] - r[k] : __longlong_as_double(0x7ff8000000000000ll);
+        }
+        double2 *rec = const_cast<double2 *>(desc_rec(a, b, s, t));
+        rec[0] = make_double2(mx, (double)e0);
+#pragma unroll
+        for (int k = 0; k < JB; ++k) rec[k + 1] = make_double2(q[2 * k], q[2 * k + 1]);
+    }
+}
+
+// Re-walk of a whole super-tile from its corrected start: segment by segment,
+// each one checked for coalescence with the stored trajectory at its start,
+// then jumped (exact release jump, its checkpoints left to comp_refill) or
+// walked.  A jump stores the segment's entry state as its first checkpoint and
+// marks it (jmark = tag, jstart); its inner checkpoints stay stale until
+// comp_refill, so a later walk of a marked segment does not compare with them.
+// The descriptor record, mark and first stored checkpoint of the next two
+// segments are loaded ahead (a chain of jumps costs no load latency per jump).
+// *nw = frames walked, *nj = frames jumped.
+template <bool BUF>
+__device__ __forceinline__ double comp_rewalk(double att, const CompArgs &a, int b, int64_t s, int len,
+                                              const BandStep &bs, bool *coalesced, int *nw, int *nj) {
+    *coalesced = false;
+    *nw = 0;
+    *nj = 0;
+    if (len <= 0) return att;
+    const int64_t cs = ck_col(a, s);
+    const int nseg = (len + SEG - 1) / SEG;
+    const double *ck = a.ck[b];
+    const uint32_t *jm = a.jmark[b];
+    auto seg_old = [&](int t) { return ck[(int64_t)(min(t, nseg - 1) * (SEG / CK_Q)) * a.RS + cs]; };
+    auto seg_mark = [&](int t) { return jm[(int64_t)min(t, nseg - 1) * a.GS + s]; };
+    SegDesc d0 = load_desc(desc_rec(a, b, s, 0)), d1 = load_desc(desc_rec(a, b, s, min(1, nseg - 1)));
+    double o0 = seg_old(0), o1 = seg_old(1);
+    uint32_t m0 = seg_mark(0), m1 = seg_mark(1);
+    for (int t = 0; t < nseg; ++t) {
+        const int i0 = t * SEG, sl = min(SEG, len - i0);
+        const int64_t sg = (int64_t)t * a.GS + s;
+        const SegDesc d2 = load_desc(desc_rec(a, b, s, min(t + 2, nseg - 1)));
+        const double o2 = seg_old(t + 2);
+        const uint32_t m2 = seg_mark(t + 2);
+        if (__double_as_longlong(o0) == __double_as_longlong(att)) {
+            *coalesced = true;
+            return att;
+        }
+        double x;
+        if (sl == SEG && a.jumps && release_jump(d0, att, &x)) {
+            a.ck[b][(int64_t)(i0 / CK_Q) * a.RS + cs] = att;  // the entry state (refill writes the rest)
+            a.jstart[b][sg] = att;
+            a.jmark[b][sg] = a.tag;
+            if (m0 != a.tag) {  // newly marked this chain: queue it for comp_refill
+                const uint32_t k = atomicAdd(a.jlist_n + b, 1u);
+                if (k < a.jlist_cap) a.jlist[b][k] = (uint32_t)sg;
+            }
+            att = x;
+            *nj += SEG;
+        } else {
+            const bool stale_inside = m0 == a.tag;  // jumped earlier this chain: inner checkpoints stale
+            if (stale_inside) a.jmark[b][sg] = 0u;  // walked now: every checkpoint rewritten below
+            bool co;
+            int w;
+            att = comp_rewalk_seg<BUF>(att, a, b, s, i0, sl, bs, &co, &w, !stale_inside);
+            *nw += w;
+            if (co) {
+                *coalesced = true;
+                return att;
+            }
+        }
+        d0 = d1;
+        d1 = d2;
+        o0 = o1;
+        o1 = o2;
+        m0 = m1;
+        m1 = m2;
+    }
+    return att;
+}
+
+// 4. speculative pass.  grid: (ceil(GS/(own*BLOCK)), 3), two waves per block:
+// wave 0 walks, wave 1 describes the same super-tiles' segments for the release
+// jumps (comp_describe; it reads the same lines of Mc, mostly from L1/L2).  Each
+// walking lane walks `own` consecutive super-tiles.  The start of the first is
+// guessed: the M of its first frame (the state tracks M closely; tools/study), or
+// with `warmup` > 0 by walking that many previous super-tiles of its chunk from
+// the M of the first warm-up frame; the later ones start from the end of the one
+// before.  Exactness never depends on the guess (the fix-up sweeps); the jumps
+// make stale stretches cheap to repair, so the default warm-up is 0.
 #ifndef MM_PASS0_BLOCK
 #define MM_PASS0_BLOCK 64
 #endif
@@ -494,13 +692,19 @@ constexpr int PASS0_BLOCK = MM_PASS0_BLOCK;
 
 // (flat column walks: the buffer-load form measured slower here, 0.27 -> 0.30 ms on
 // C2, though it helps the sweeps' lone walkers)
-__global__ void __launch_bounds__(PASS0_BLOCK) comp_pass0_kernel(CompArgs a) {
-    const int64_t L = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // lane j of chunk c
+__global__ void __launch_bounds__(2 * PASS0_BLOCK) comp_pass0_kernel(CompArgs a) {
+    const bool describer = threadIdx.x >= PASS0_BLOCK;
+    const int64_t L = (int64_t)blockIdx.x * PASS0_BLOCK + (threadIdx.x % PASS0_BLOCK);  // lane j of chunk c
     const int b = blockIdx.y;
     const int64_t c = L / a.ocols, j = L - c * a.ocols;
     if (c * a.SPC >= a.GS) return;
     const int64_t s0 = c * a.SPC + j * a.own, s1 = c * a.SPC + min(j * a.own + a.own, a.SPC);
     const BandStep bs = band_step(a, b);
+    if (describer) {
+        if (a.jumps)
+            for (int64_t s = s0; s < s1; ++s) comp_describe(a, b, s, super_of(a, b, s).len, bs);
+        return;
+    }
     double att = 0.0;
     bool warm = false;
     for (int64_t s = s0; s < s1; ++s) {
@@ -517,7 +721,7 @@ __global__ void __launch_bounds__(PASS0_BLOCK) comp_pass0_kernel(CompArgs a) {
             att = a.Mc[b][cm_col(a, w0)];  // row 0 of super-tile w0
             for (int64_t w = w0; w < s; ++w) att = comp_walk<false>(att, a, b, w, a.U, bs);
         } else if (!warm) {
-            att = 0.0;
+            att = a.Mc[b][cm_col(a, s)];  // the M of its first frame
         }
         a.start[b][s] = att;
         att = comp_walk<true>(att, a, b, s, st.len, bs);
@@ -549,6 +753,14 @@ __device__ __forceinline__ bool comp_claim(const CompArgs &a, int b, int64_t s) 
            a.stamp;
 }
 
+// Sweep 1 (a.heads == 0) is a Jacobi step: every stale super-tile re-walks from
+// its predecessor's current end.  Later sweeps start a walker only at the HEAD of
+// each run of consecutive stale super-tiles (its predecessor is not stale): the
+// head's walker carries its value through the run by continuation, where Jacobi
+// walkers inside the run would claim the run's super-tiles first and stop the
+// correction after one super-tile per sweep.  Every lane that sees its super-tile
+// stale flags the sweep, so a sweep that flags nothing saw every start equal to
+// its predecessor's end and changed nothing (the fixed point: exact).
 template <bool BUF>
 __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned int *prev_changed) {
     if (prev_changed && *prev_changed == 0u) return;
@@ -560,29 +772,55 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
     double *end = a.end[b];
     double att = ld_sc1(end + s - 1);
     if (__double_as_longlong(att) == __double_as_longlong(a.start[b][s])) return;
+    *a.changed = 1u;  // stale: the next sweep re-checks (benign race: every writer stores 1)
+    if (a.heads && st.p0 > 0 && (st.p0 / a.U) > 1) {  // the predecessor is not a chunk start
+        const double pe = ld_sc1(end + s - 2);
+        if (__double_as_longlong(pe) != __double_as_longlong(a.start[b][s - 1])) return;  // inside a run
+    }
     if (!comp_claim(a, b, s)) return;  // a walker continuing from s - 1 owns it
     const BandStep bs = band_step(a, b);
-    unsigned long long walked = 0;
+    unsigned long long walked = 0, jumped = 0;
     int64_t cur = s;
     for (;;) {
         a.start[b][cur] = att;
         bool coalesced;
-        int nw;
-        const double t = comp_rewalk<BUF>(att, a, b, cur, st.len, bs, &coalesced, &nw);
+        int nw, nj;
+        const double t = comp_rewalk<BUF>(att, a, b, cur, st.len, bs, &coalesced, &nw, &nj);
         walked += nw;
+        jumped += nj;
         if (coalesced) break;
         st_sc1(end + cur, t);
         if (st.last) break;  // the chunk's last super-tile: no successor
         const int64_t nxt = cur + 1;
-        if (!comp_claim(a, b, nxt)) {
-            *a.changed = 1u;  // benign race: every writer stores 1
-            break;
-        }
+        if (!comp_claim(a, b, nxt)) break;  // its owner read an older end of cur: it is stale (flagged) next sweep
         att = t;
         cur = nxt;
         st = super_of(a, b, cur);
     }
     atomicAdd(a.walked, walked);
+    if (jumped) atomicAdd(a.walked + 1, jumped);
+}
+
+// 6. checkpoints of the segments the sweeps jumped over.  grid (n, 3): the lanes
+// of band blockIdx.y stride over its list of segments newly marked this chain
+// (or, if the list overflowed, over all its segments) and re-walk each one still
+// marked with this chain's tag (a segment walked again after its jump was
+// unmarked by that walk) from its recorded exact entry state.  The band is
+// uniform per block: the walks' buffer descriptors stay scalar.
+template <bool BUF>
+__global__ void __launch_bounds__(64) comp_refill_kernel(CompArgs a) {
+    const int b = blockIdx.y;
+    const uint32_t n = a.jlist_n[b];
+    const int64_t NG = (int64_t)a.SPT * a.GS;
+    const bool all = n > a.jlist_cap;
+    const int64_t total = all ? NG : (int64_t)n;
+    const BandStep bs = band_step(a, b);
+    for (int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 64) {
+        const int64_t sg = all ? i : (int64_t)a.jlist[b][i];
+        if (a.jmark[b][sg] != a.tag) continue;
+        const int64_t t = sg / a.GS, s = sg - t * a.GS;
+        comp_walk<true, BUF>(a.jstart[b][sg], a, b, s, SEG, bs, (int)t * SEG);
+    }
 }
 
 // compacted index p of chunk c -> element address in the super-tile-major array

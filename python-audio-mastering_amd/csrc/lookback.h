@@ -20,10 +20,13 @@
 //
 // Logical block order comes from an atomic ticket, so a block only ever waits
 // on blocks that started before it (no dispatch-order assumption).  Handed-off
-// words are stored and loaded with agent-scope relaxed atomics (sc1) and the
-// status words are zeroed by a hipMemsetAsync before every launch
-// (cdna_hip_programming.md Guideline 16, R1).  Spins are bounded: on timeout
-// the kernel records an error word and proceeds (the host reports it).
+// words are stored with agent-scope relaxed atomics (sc1, write-through), every
+// storing wave drains them (vmcnt(0)) before the workgroup barrier behind which
+// one lane stores the status word; the consumer wave polls relaxed, then takes
+// ONE agent-scope acquire before loading the payload (cdna_hip_programming.md
+// Guideline 16: producer R1, consumer poll -> acquire -> loads).  Status words
+// are zeroed by a hipMemsetAsync before every launch.  Spins are bounded: on
+// timeout the kernel records an error word and proceeds (the host reports it).
 #pragma once
 #include "common.h"
 
@@ -215,7 +218,12 @@ __device__ void lb_carry(const LbArgs &a, int blk, int t, int c, bool valid, boo
                     }
                 }
             }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // agent-scope acquire after the polls (cdna_hip_programming.md Guideline 16:
+            // ONE relaxed poll, ONE agent acquire, then the loads): this CU's L1 holds
+            // no stale copy of a predecessor's aggregate or prefix, whatever the
+            // placement.  The payload loads below stay sc1 (L2-served) as well.
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const unsigned long long m = __ballot(st == 2u);
             const int first = m ? __builtin_ctzll(m) : LB_WIN;  // lanes <= first contribute
 #pragma unroll 1

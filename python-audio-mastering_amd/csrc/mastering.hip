@@ -63,8 +63,7 @@ struct mm_ctx {
     char *ctl = nullptr;                // the chain's control block (setup_control)
     uint32_t *ctl_claims = nullptr;     // its zeroed claim stamps
     int comp_iters = 0, comp_pending = 0;
-    int comp_hint = 0;  // sweeps the last converged solve of this context needed, + 1 (0: none yet)
-    int warm_extra = 0;  // adaptive warm-up: super-tiles added to the job's (evaluate_chain)
+    uint32_t chain_tag = 0;  // per-chain tag of the release-jump marks (compressor.hip)
     unsigned comp_nb = 0;
     // loudness on the device
     double *gate_out = nullptr;         // [2]: L, gain
@@ -81,7 +80,7 @@ struct mm_ctx {
     std::map<std::string, KStat> stats;
     std::vector<std::string> stat_order;
     // host tables already resident on the device
-    const double *lut_src[3] = {nullptr, nullptr, nullptr};  // host tables already on the device
+    uint64_t lut_key[3] = {0, 0, 0};  // content keys of the band tables on the device (0: none)
     std::map<std::string, std::vector<double>> mats_cache;
     // pinned block the chain's results are copied into (one sync per chain)
     char *rb = nullptr;
@@ -113,6 +112,12 @@ static int set_err(mm_ctx *c, int code, const char *fmt, ...) {
                            __FILE__, __LINE__);                                              \
     } while (0)
 
+#define RET_EARLY(expr)             \
+    do {                            \
+        int r_ = (expr);            \
+        if (r_ != MM_OK) return r_; \
+    } while (0)
+
 template <typename T>
 static int get_buf(mm_ctx *c, const char *name, size_t count, T **out) {
     DevBuf &b = c->bufs[name];
@@ -125,6 +130,15 @@ static int get_buf(mm_ctx *c, const char *name, size_t count, T **out) {
         b.cap = bytes;
     }
     *out = reinterpret_cast<T *>(b.p);
+    return MM_OK;
+}
+
+// get_buf whose storage is zeroed (on the stream) whenever it is (re)allocated
+template <typename T>
+static int get_buf_zeroed(mm_ctx *c, const char *name, size_t count, T **out) {
+    const size_t before = c->bufs[name].cap;
+    RET_EARLY(get_buf(c, name, count, out));
+    if (c->bufs[name].cap != before) HIPCHK(c, hipMemsetAsync(*out, 0, c->bufs[name].cap, c->stream));
     return MM_OK;
 }
 
@@ -303,9 +317,7 @@ static int launch_eq(mm_ctx *c, int nsec, int ch, unsigned nblk, const EqArgs &e
 // successor may be stale) and exits at once if sweep k-1 flagged nothing.
 // Convergence is checked at the chain's single sync (evaluate_chain); a rare
 // unconverged batch is extended there (MM_COMP_SWEEPS sets the queued count).
-constexpr int COMP_SWEEPS = 6;  // queued by a context's first chain; later ones follow comp_hint
-constexpr int WARM_EXTRA = 6;   // adaptive warm-up step (super-tiles)
-constexpr int WARM_ADAPT_MIN = 4;  // jobs with a shorter warm-up (tests of the resume path) are left as set
+constexpr int COMP_SWEEPS = 4;  // queued per chain (a sweep after a quiet one exits at once)
 
 static int comp_sweeps(mm_ctx *c, int n) {
     CompArgs &ca = c->ca;
@@ -315,6 +327,7 @@ static int comp_sweeps(mm_ctx *c, int n) {
     c->comp_flags_fresh = false;
     for (int k = 0; k < n; ++k) {
         ca.stamp = ++c->comp_stamp;
+        ca.heads = ca.stamp > 1 ? 1 : 0;  // the chain's first sweep is a Jacobi step
         ca.changed = c->comp_changed + k;
         const unsigned int *prevf = k > 0 ? c->comp_changed + (k - 1) : nullptr;
         if (ca.buf_ok) RET(launch(c, "comp_fix", comp_fix_kernel<true>, dim3(blocks_for(NS, 64), 3), dim3(64), 0, ca, prevf));
@@ -327,13 +340,19 @@ static int comp_sweeps(mm_ctx *c, int n) {
 // gains + overlay into q2, every tile starting from the walkers' checkpoints
 static int comp_back(mm_ctx *c) {
     const CompArgs &ca = c->ca;
+    // checkpoints of the segments the sweeps jumped over, then the gains
+    // grid-stride over each band's marked segments: enough lanes that a heavily
+    // jumped solve (P_HOT: tens of thousands of segments) refills in one pass
+    const dim3 gr((unsigned)std::min<int64_t>(1024, std::max<int64_t>(16, (int64_t)ca.SPT * ca.GS / 64)), 3);
+    if (ca.buf_ok) RET(launch(c, "comp_refill", comp_refill_kernel<true>, gr, dim3(64), 0, ca));
+    else RET(launch(c, "comp_refill", comp_refill_kernel<false>, gr, dim3(64), 0, ca));
     return launch(c, "comp_apply", comp_apply_kernel, dim3(blocks_for(ca.G, APPLY_TILES)), dim3(3 * APPLY_TILES), 0,
                   ca);
 }
 
 // Pinned readback block of one chain pass (offsets in bytes): look-back error
 // word, sweep flags, re-walked frame count, loudness + gain, per-chunk active counts.
-constexpr size_t RB_ERR = 0, RB_FLAGS = 16, RB_WALKED = 80, RB_LG = 96, RB_TOTALS = 128;
+constexpr size_t RB_ERR = 0, RB_FLAGS = 16, RB_WALKED = 80, RB_LG = 96, RB_JLIST = 112, RB_TOTALS = 128;
 static size_t rb_bytes(int64_t nch) { return RB_TOTALS + (size_t)12 * nch; }
 
 static int ensure_rb(mm_ctx *c, size_t bytes) {
@@ -362,6 +381,10 @@ static int queue_readback(mm_ctx *c, bool lufs) {
 // block only waits on blocks that started before it) and whether the queued
 // sweeps converged.
 static int evaluate_chain(mm_ctx *c, bool *converged) {
+    if (getenv("MM_DEBUG_JLIST"))
+        fprintf(stderr, "jlist_n=%u walked=%llu jumped=%llu\n", reinterpret_cast<const unsigned *>(c->rb + RB_JLIST)[0],
+                *reinterpret_cast<const unsigned long long *>(c->rb + RB_WALKED),
+                *reinterpret_cast<const unsigned long long *>(c->rb + RB_WALKED + 8));
     if (*reinterpret_cast<const unsigned *>(c->rb + RB_ERR)) return set_err(c, MM_ERR_STATE, "IIR look-back timed out");
     *converged = true;
     if (c->comp_on && c->comp_pending) {
@@ -371,21 +394,6 @@ static int evaluate_chain(mm_ctx *c, bool *converged) {
         c->comp_iters += k;
         *converged = k < c->comp_pending;
         c->comp_pending = 0;
-        if (*converged) {
-            c->comp_hint = std::max(2, std::min(16, c->comp_iters + 2));
-            // Adaptive warm-up (jobs at the default warm-up or more): heavily
-            // compressed material coalesces late, so a solve that
-            // re-walked over 1 % of its active frames raises the next solve's
-            // warm-up by WARM_EXTRA super-tiles, and one that re-walked under
-            // 0.02 % drops it again (C2 at P_HOT: 2.52 -> 2.01 ms; P_FULL keeps 6,
-            // where 9 costs 6 %).
-            int64_t active = 0;
-            const int32_t *tot = reinterpret_cast<const int32_t *>(c->rb + RB_TOTALS);
-            for (int64_t k = 0; k < 3 * comp_chunks(c); ++k) active += tot[k];
-            const double walked = (double)*reinterpret_cast<const unsigned long long *>(c->rb + RB_WALKED);
-            if (walked > 0.01 * (double)active) c->warm_extra = WARM_EXTRA;
-            else if (walked < 2e-4 * (double)active) c->warm_extra = 0;
-        }
         if (!*converged && c->comp_iters >= c->job.comp_max_iters)
             return set_err(c, MM_ERR_STATE, "compressor did not converge in %d sweeps", c->comp_iters);
     }
@@ -402,8 +410,8 @@ static int chain_check(mm_ctx *c, bool *converged) {
 // SPC super-tiles reserved per chunk, nch chunks.
 static void comp_geometry(const mm_job *j, int64_t G, int *U, int64_t *SPC, int64_t *nch) {
     const int K = j->tiles_per_chunk;
-    *U = std::max(16, std::min(j->comp_super, FIX_MAX_U));
-    *U -= *U % CK_Q;
+    *U = std::max(SEG, std::min(j->comp_super, FIX_MAX_U));
+    *U -= *U % SEG;  // whole jump segments (SEG is a multiple of CK_Q and WALK_WB)
     *nch = (G + K - 1) / K;
     *SPC = ((int64_t)K * j->tile + *U - 1) / *U;
 }
@@ -449,7 +457,7 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     ca.T = T;
     ca.K = K;
     ca.ch = ch;
-    ca.warmup = j->comp_warmup + (j->comp_warmup >= WARM_ADAPT_MIN ? c->warm_extra : 0);
+    ca.warmup = j->comp_warmup;
     int64_t nchunks;
     comp_geometry(j, G, &ca.U, &ca.SPC, &nchunks);
     ca.GS = nchunks * ca.SPC;
@@ -458,10 +466,13 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     RET(get_buf(c, "q2", TG, &q2));
     ca.q_out = q2;
     *q2_out = q2;
-    // pass-0 ownership: enough lanes for the chip at C2 size (2 super-tiles per lane),
-    // more per lane on bigger problems and when batch streams run beside this one
+    // pass-0 ownership: one super-tile per lane without a warm-up; with one, enough
+    // lanes for the chip at C2 size (2 super-tiles per lane: the warm-up's M re-reads
+    // halve), more per lane on bigger problems and when batch streams run beside
+    // this one; MM_PASS0_OWN for experiments
     ca.own = c->own_override > 0 ? c->own_override
-                                 : (int)std::max<int64_t>(1, std::min<int64_t>(4, (NS * c->concurrency + 3307) / 6615));
+             : ca.warmup == 0   ? 1
+                                : (int)std::max<int64_t>(1, std::min<int64_t>(4, (NS * c->concurrency + 3307) / 6615));
     ca.ocols = (ca.SPC + ca.own - 1) / ca.own;
     ca.RS = ca.ocols * ca.own;
     const int64_t RS = ca.RS;
@@ -475,6 +486,20 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     ca.CKB = RS * ck_rows;
     RET(get_buf(c, "comp_ck", (size_t)3 * nchunks * ca.CKB, &cks));
     RET(get_buf(c, "comp_lut", (size_t)3 * 32769, &luts));
+    ca.SPT = ca.U / SEG;
+    const int64_t NG = (int64_t)ca.SPT * NS;  // jump segments per band
+    double *desc, *jst;
+    uint32_t *jmark;
+    RET(get_buf(c, "comp_desc", (size_t)3 * DREC * NG, &desc));
+    RET(get_buf(c, "comp_jstart", (size_t)3 * NG, &jst));
+    RET(get_buf_zeroed(c, "comp_jmark", (size_t)3 * NG, &jmark));  // tags of earlier chains never match
+    uint32_t *jlist;
+    RET(get_buf(c, "comp_jlist", (size_t)3 * NG, &jlist));
+    ca.jlist_cap = (uint32_t)std::min<int64_t>(NG, 0xffffffffll);
+    ca.jlist_n = reinterpret_cast<uint32_t *>(c->ctl + RB_JLIST);  // zeroed with the control block
+    if (++c->chain_tag == 0) ++c->chain_tag;
+    ca.tag = c->chain_tag;
+    ca.jumps = getenv("MM_COMP_NOJUMP") ? 0 : 1;  // diagnostics: results must not change
     unsigned int *changed = c->comp_changed;  // zeroed with the chain's control words
     ca.walked = reinterpret_cast<unsigned long long *>(c->ctl + RB_WALKED);
     int32_t *cnt, *off, *tot;
@@ -495,13 +520,14 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
         ca.Mc[b] = mcb;
         ca.band[b] = bands[b];
         ca.lut[b] = luts + (size_t)b * 32769;
-        // tables are immutable host arrays owned by the caller's job: upload once
-        if (c->lut_src[b] != j->band[b].lut) {
+        // cached by content key (a host pointer may be reused by another table once the
+        // caller frees one): upload when the key differs or is unknown
+        if (j->band[b].lut_key == 0 || c->lut_key[b] != j->band[b].lut_key) {
             // the M column of the host's {M, M/A, M/R, 0} rows
             HIPCHK(c, hipMemcpy2DAsync(luts + (size_t)b * 32769, sizeof(double), j->band[b].lut,
                                        4 * sizeof(double), sizeof(double), 32769, hipMemcpyHostToDevice,
                                        c->stream));
-            c->lut_src[b] = j->band[b].lut;
+            c->lut_key[b] = j->band[b].lut_key;
         }
         ca.r0[b] = (uint32_t)j->band[b].r0;
         ca.look[b] = j->band[b].look;
@@ -516,6 +542,10 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
         ca.ck[b] = cks + (size_t)b * nchunks * ca.CKB;
         ca.end[b] = ends + (size_t)b * NS;
         ca.claim[b] = claims + (size_t)b * NS;
+        ca.desc[b] = desc + (size_t)b * DREC * NG;
+        ca.jstart[b] = jst + (size_t)b * NG;
+        ca.jmark[b] = jmark + (size_t)b * NG;
+        ca.jlist[b] = jlist + (size_t)b * NG;
     }
     RET(launch(c, "comp_rms", comp_rms_kernel, dim3(nb, 3), dim3(256), 0, ca));
     RET(launch(c, "comp_offsets", comp_offsets_kernel, dim3((unsigned)nchunks, 3), dim3(1024), 0, ca));
@@ -528,7 +558,7 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
         ca.ck_bytes = ca.buf_ok ? (uint32_t)ckb : 0u;
     }
     const dim3 g0(blocks_for(nchunks * ca.ocols, PASS0_BLOCK), 3);
-    RET(launch(c, "comp_pass0", comp_pass0_kernel, g0, dim3(PASS0_BLOCK), 0, ca));
+    RET(launch(c, "comp_pass0", comp_pass0_kernel, g0, dim3(2 * PASS0_BLOCK), 0, ca));
     c->comp_on = true;
     c->ca = ca;
     c->comp_stamp = 0;
@@ -538,7 +568,7 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     c->comp_nb = nb;
     // as many as the last solve on this context needed (+ 1 spare): a stream of similar
     // batches queues no idle sweeps and rarely resumes from the host
-    int sweeps = c->comp_hint > 0 ? c->comp_hint : COMP_SWEEPS;
+    int sweeps = COMP_SWEEPS;
     if (const char *e = getenv("MM_COMP_SWEEPS")) sweeps = std::max(1, std::min(16, atoi(e)));  // tests / tuning
     RET(comp_sweeps(c, sweeps));
     RET(comp_back(c));
@@ -839,6 +869,7 @@ static int complete_chain(mm_ctx *c, const mm_job *j, void *d_out, mm_result *re
         const int32_t *tot = reinterpret_cast<const int32_t *>(c->rb + RB_TOTALS);
         for (int64_t k = 0; k < 3 * comp_chunks(c); ++k) res->comp_active += tot[k];
         res->comp_walked = c->comp_on ? (int64_t) * reinterpret_cast<const unsigned long long *>(c->rb + RB_WALKED) : 0;
+        res->comp_jumped = c->comp_on ? (int64_t) * reinterpret_cast<const unsigned long long *>(c->rb + RB_WALKED + 8) : 0;
     }
     return MM_OK;
 }
@@ -906,7 +937,10 @@ static bool fusable(const mm_job *J, int n) {
                 if (x.thresh_rms != y.thresh_rms || x.attack_frames != y.attack_frames ||
                     x.release_frames != y.release_frames || x.look != y.look || x.r0 != y.r0)
                     return false;
-                if (x.lut != y.lut && memcmp(x.lut, y.lut, (size_t)32769 * 4 * sizeof(double)) != 0) return false;
+                const bool keyed = x.lut_key != 0 && y.lut_key != 0;
+                if (keyed ? x.lut_key != y.lut_key
+                          : (x.lut != y.lut && memcmp(x.lut, y.lut, (size_t)32769 * 4 * sizeof(double)) != 0))
+                    return false;
             }
         }
     }
@@ -1103,6 +1137,7 @@ static int fused_complete(mm_ctx *c, int n, const mm_job *J, void *const *d_out,
     const int64_t nchk = comp_chunks(c), CF = (int64_t)j0.tile * j0.tiles_per_chunk;
     const int32_t *tot = reinterpret_cast<const int32_t *>(c->rb + RB_TOTALS);
     const int64_t walked = c->comp_on ? (int64_t) * reinterpret_cast<const unsigned long long *>(c->rb + RB_WALKED) : 0;
+    const int64_t jumped = c->comp_on ? (int64_t) * reinterpret_cast<const unsigned long long *>(c->rb + RB_WALKED + 8) : 0;
     for (int i = 0; i < n; ++i) {
         mm_result &r = res[i];
         r.loudness = lufs ? l2[2 * i] : NAN;
@@ -1112,7 +1147,10 @@ static int fused_complete(mm_ctx *c, int n, const mm_job *J, void *const *d_out,
         r.comp_active = 0;
         for (int b = 0; b < 3 && c->comp_on; ++b)
             for (int64_t k = p.off[i] / CF; k < p.off[i + 1] / CF; ++k) r.comp_active += tot[b * nchk + k];
-        r.comp_walked = walked;  // unit total
+        // the unit's solve statistics are reported once, on its first track (sums over
+        // a batch's results then count every unit once)
+        r.comp_walked = i == 0 ? walked : 0;
+        r.comp_jumped = i == 0 ? jumped : 0;
     }
     return MM_OK;
 }

@@ -18,7 +18,7 @@ Reference anchors (worker/audio_mastering_engine.py = "AME"):
 from __future__ import annotations
 
 import functools
-import os
+import hashlib
 import math
 
 import numpy as np
@@ -26,8 +26,7 @@ import scipy.signal
 
 MAX_DIM = 8
 CHUNK_MS = 30 * 1000  # AME:48
-DEFAULT_TILE = int(os.environ.get("MM_TILE", "125"))  # divides 30 s chunks at every rate that is a multiple
-                                                     # of 25 Hz (MM_TILE: tuning experiments)
+DEFAULT_TILE = 125     # divides 30 s chunks at every rate that is a multiple of 25 Hz
 OPS_TILE = 125         # tile of the per-stage operators' look-back tables (== OPS_TILE in csrc/ops.hip)
 
 EQ_KEYS = ("bass_boost", "mid_cut", "presence_boost", "treble_boost")
@@ -85,7 +84,8 @@ def check_chunk_geometry(bounds, nominal: int, rate: int, multiband: bool):
                 raise NotImplementedError(f"pydub overlay re-slicing changes a chunk's length at {rate} Hz")
 
 
-def choose_tile(chunk_frames: int, preferred: int = DEFAULT_TILE) -> int:
+def choose_tile(chunk_frames: int, preferred: int | None = None) -> int:
+    preferred = preferred or DEFAULT_TILE
     if chunk_frames % preferred == 0:
         return preferred
     best = 0
@@ -276,12 +276,22 @@ def step_table(threshold, ratio, attack_frames, release_frames):
     return out
 
 
+@functools.lru_cache(maxsize=64)
+def table_key(threshold, ratio):
+    """Content key of max_att_table(threshold, ratio) (nonzero 64-bit): the device
+    caches a band's table by this key, not by the host pointer, whose memory an
+    evicted table may hand to a different one."""
+    M, _ = max_att_table(threshold, ratio)
+    return int.from_bytes(hashlib.blake2b(M.tobytes(), digest_size=8).digest(), "little") | 1
+
+
 def band_constants(rate, threshold, ratio, attack, release):
     table, thr = max_att_table(float(threshold), float(ratio))
     af = attack * (rate / 1000.0)
     rf = release * (rate / 1000.0)
     return {"table": table, "thresh_rms": thr, "attack_frames": af, "release_frames": rf, "look": int(af),
-            "lut": step_table(float(threshold), float(ratio), af, rf)}
+            "lut": step_table(float(threshold), float(ratio), af, rf),
+            "lut_key": table_key(float(threshold), float(ratio))}
 
 
 # ---------------------------------------------------- loudness block geometry

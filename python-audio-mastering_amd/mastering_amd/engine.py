@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import ctypes
 import functools
+import math
 import os
 
 import numpy as np
@@ -29,17 +30,22 @@ EQ_PRESETS = {
              "description": "Warm low-mids for guitars and punchy presence for snare/vocals."},
 }
 
-COMP_WARMUP = int(os.environ.get("MM_COMP_WARMUP", "6"))  # super-tiles of warm-up walk before each one
+COMP_WARMUP = 6  # super-tiles of speculative warm-up walk before each one (fixed: no per-context history)
 COMP_MAX_ITERS = 100000
-# envelope solve unit in active frames at 44.1 kHz (MM_COMP_SUPER overrides).  The
-# envelope's time constants are in ms (attack/release frames scale with the rate),
-# so the trajectories' coalescence lengths scale with the rate too: the unit does.
-COMP_SUPER_FRAMES = int(os.environ.get("MM_COMP_SUPER", "1000"))
+# envelope solve unit in active frames at 44.1 kHz.  The envelope's time constants
+# are in ms (attack/release frames scale with the rate), so the unit scales with it.
+COMP_SUPER_FRAMES = 1000
+COMP_SEG = 100  # release-jump segment of the envelope solve (== SEG in csrc/compressor.hip)
 
 
-def comp_super_frames(rate: int) -> int:
-    """Super-tile length (active frames, a multiple of 8) for `rate`."""
-    return max(64, int(round(COMP_SUPER_FRAMES * rate / 44100 / 8)) * 8)
+def comp_super_frames(rate: int, tile: int = design.DEFAULT_TILE) -> int:
+    """Super-tile length for `rate`: whole jump segments, and whole tiles where the
+    two align (the compaction's stores stay in few lines when super-tile bounds fall
+    on tile bounds: DESIGN.md §8)."""
+    unit = COMP_SEG * tile // math.gcd(COMP_SEG, tile)
+    if unit > COMP_SUPER_FRAMES:
+        unit = COMP_SEG
+    return max(unit, int(round(COMP_SUPER_FRAMES * rate / 44100 / unit)) * unit)
 
 
 class Job:
@@ -113,9 +119,10 @@ class Job:
                 nz = np.flatnonzero(tab[:, 0])
                 jb.r0 = int(nz[0]) if nz.size else 32769
                 jb.lut = tab.ctypes.data_as(native.c_double_p)
+                jb.lut_key = bc["lut_key"]
         j.comp_warmup = COMP_WARMUP
         j.comp_max_iters = COMP_MAX_ITERS
-        j.comp_super = comp_super_frames(self.rate)
+        j.comp_super = comp_super_frames(self.rate, self.tile)
         # --- loudness
         if lufs is not None:
             self._fill_iir(j.kweight, design.kweight_sections(self.rate), [2], self.tile, design.LB_THREADS)
@@ -174,6 +181,7 @@ def _info(job: "Job", res: native.MMResult) -> dict:
     return {"loudness": res.loudness if job.job.lufs_on else None,
             "gain_db": (float(job.job.lufs_target) - res.loudness) if job.job.lufs_on else None,
             "gain_linear": res.gain_linear, "frames": job.frames_proc, "comp_iters": res.comp_iters,
+            "comp_walked": res.comp_walked, "comp_jumped": res.comp_jumped, "comp_active": res.comp_active,
             "chunks": len(job.chunks), "tile": job.tile}
 
 

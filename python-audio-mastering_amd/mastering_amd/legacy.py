@@ -156,6 +156,9 @@ def apply_multiband_compressor(chunk, settings, frame_rate=None, device: int = 0
         ctx.check(ctx.lib.mm_op_compress_bands(ctx.ptr, ctypes.byref(job.job), ops._ptr(bands[0]), ops._ptr(bands[1]),
                                                ops._ptr(bands[2]), ops._ptr(mix)), "mm_op_compress_bands")
     n1 = design.pydub_frame(design.pydub_len_ms(n, rate), rate)  # pydub overlay's ms re-slicing
+    n2 = design.pydub_frame(design.pydub_len_ms(n1, rate), rate)  # the second overlay re-slices again
+    if n2 != n1:
+        raise NotImplementedError(f"pydub overlay re-slicing is not stable at {rate} Hz")
     if n1 != n:
         out = np.zeros((n1,) + pcm.shape[1:], np.int16)
         out[:min(n, n1)] = mix[:min(n, n1)]
@@ -190,7 +193,10 @@ def master_pcm(pcm: np.ndarray, rate: int, settings: dict, device: int = 0) -> n
     settings = dict(settings or {})
     n = pcm.shape[0]
     chunks = []
-    for a, b in design.chunk_bounds(n, rate):
+    bounds = design.chunk_bounds(n, rate)
+    if settings.get("use_multiband"):  # the overlay's ms re-slicing must keep every chunk's length
+        design.check_chunk_geometry(bounds, design.pydub_frame(design.CHUNK_MS, rate), rate, True)
+    for a, b in bounds:
         c = pcm[a:min(b, n)]
         if b > n:  # pydub pads <= 2 ms of silence
             c = np.concatenate([c, np.zeros((b - n,) + pcm.shape[1:], np.int16)])

@@ -36,7 +36,7 @@ class MMIir(ctypes.Structure):
 class MMBand(ctypes.Structure):
     _fields_ = [("thresh_rms", ctypes.c_double), ("attack_frames", ctypes.c_double),
                 ("release_frames", ctypes.c_double), ("look", ctypes.c_int32), ("r0", ctypes.c_int32),
-                ("lut", c_double_p)]
+                ("lut", c_double_p), ("lut_key", ctypes.c_uint64)]
 
 
 class MMJob(ctypes.Structure):
@@ -56,7 +56,8 @@ class MMJob(ctypes.Structure):
 class MMResult(ctypes.Structure):
     _fields_ = [("loudness", ctypes.c_double), ("gain_linear", ctypes.c_double), ("frames_out", ctypes.c_int64),
                 ("comp_iters", ctypes.c_int32), ("_pad", ctypes.c_int32),
-                ("comp_active", ctypes.c_int64), ("comp_walked", ctypes.c_int64)]
+                ("comp_active", ctypes.c_int64), ("comp_walked", ctypes.c_int64),
+                ("comp_jumped", ctypes.c_int64)]
 
 
 class MMWavInfo(ctypes.Structure):

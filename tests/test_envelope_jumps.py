@@ -1,0 +1,121 @@
+"""The envelope solve's release jumps (csrc/compressor.hip comp_describe /
+release_jump) restated in Python and checked on the CPU: every jump
+the device would take lands bit for bit on the state pydub's step-by-step loop
+reaches (AME:207-209).
+
+The compacted M sequences come from the oracle's own band split of a pink-noise
+track at P_HOT thresholds (every envelope branch fires), so the check covers
+long release stretches, parity ties and binade crossings of real trajectories."""
+import math
+import struct
+
+import numpy as np
+import pytest
+
+from mastering_amd import design
+
+SEG, JB = 100, 4  # == csrc/compressor.hip
+MANT = (1 << 52) - 1
+NAN = float("nan")
+
+
+def _bits(x):
+    return struct.unpack("<Q", struct.pack("<d", x))[0]
+
+
+def _from(b):
+    return struct.unpack("<d", struct.pack("<Q", b))[0]
+
+
+def _step(a, m, A, R):
+    """pydub's update (Appendix A); M/A, M/R correctly rounded like the device's."""
+    inc, dec = m / A, m / R
+    if a <= m:
+        return min(a + inc, m)
+    return max(a - dec, 0.0)
+
+
+def _describe(M, R):
+    """comp_describe for one segment: (max M, e0, q[2 JB])."""
+    e0 = (_bits(M[0]) >> 52) - 1023
+    r0 = [_from(((e0 + k // 2 + 1023) << 52) | (MANT - 63 + k % 2)) for k in range(2 * JB)]
+    r = list(r0)
+    for m in M:
+        dec = m / R
+        r = [x - dec for x in r]
+    q = []
+    for k in range(2 * JB):
+        rb = _bits(r[k])
+        ok = (rb >> 52) == e0 + k // 2 + 1023 and (rb & MANT) != 0
+        q.append(r0[k] - r[k] if ok else NAN)
+    return max(M), e0, q
+
+
+def _jump(desc, att):
+    """release_jump: the state after the segment, or None."""
+    mx, e0, q = desc
+    if not att > 0.0:
+        return None
+    ab = _bits(att)
+    k = (ab >> 52) - 1023 - e0
+    if k < 0 or k >= JB:
+        return None
+    x = att - q[2 * k + (ab & 1)]
+    if math.isnan(x):
+        return None
+    xb = _bits(x)
+    if not x > mx or (xb >> 52) != (ab >> 52) or (xb & MANT) == 0:
+        return None
+    return x
+
+
+def _band_M(seconds=20):
+    import bench
+    from mastering_amd.synth import pink_noise_pcm16
+    from oracle import mastering_oracle as mo
+    rate, st = 44100, bench.P_HOT
+    pcm = pink_noise_pcm16(seconds * rate, rate, 2, track=7)
+    x = mo.stereo_width(mo.equalize(mo.saturation(mo.pcm_to_float(pcm), st["saturation"]), rate, st), st["width"])
+    thr, rat = mo.multiband_params(st)
+    out = []
+    for band, t, r, (at, rel) in zip(mo.band_split(mo.quantize(x), rate), thr, rat, mo.BAND_TIMES):
+        bc = design.band_constants(rate, t, r, at, rel)
+        e2 = (band.astype(np.int64) ** 2).sum(axis=1)
+        cs = np.concatenate([[0], np.cumsum(e2)])
+        i = np.arange(band.shape[0])
+        lo = np.maximum(i - bc["look"], 0)
+        n = (i - lo) * 2
+        S = cs[i] - cs[lo]
+        rms = np.zeros(band.shape[0], np.int64)
+        nz = n > 0
+        rms[nz] = np.floor(np.sqrt(S[nz] / n[nz])).astype(np.int64)  # == audioop.rms (test_oracle.py)
+        M = bc["table"][np.minimum(rms, 32768)]
+        out.append((M[M != 0], bc["attack_frames"], bc["release_frames"]))
+    return out
+
+
+@pytest.mark.timeout(300)
+def test_release_jumps_are_exact():
+    jumps = checked = 0
+    for M, A, R in _band_M():
+        traj = [0.0]
+        for m in M:
+            traj.append(_step(traj[-1], m, A, R))
+        for s0 in range(0, len(M) - SEG + 1, SEG):
+            seg = [float(v) for v in M[s0:s0 + SEG]]
+            desc = _describe(seg, R)
+            true = traj[s0]
+            # the true state, its neighbours (other parity / rounding), and states in
+            # the descriptor's other binades
+            for att in (true, math.nextafter(true, math.inf), math.nextafter(true, -math.inf), true * 1.5,
+                        desc[0] * 1.0001, desc[0] * 2.01, desc[0] * 4.3):
+                checked += 1
+                x = _jump(desc, att)
+                if x is None:
+                    continue
+                jumps += 1
+                y = att
+                for m in seg:
+                    y = _step(y, m, A, R)
+                assert x == y, (s0, att, x, y)
+    assert jumps > 0.3 * checked, (jumps, checked)  # the jump conditions are not vacuous
