@@ -137,6 +137,9 @@ int mm_destroy(mm_ctx *ctx);
 const char *mm_last_error(mm_ctx *ctx);
 int mm_sync(mm_ctx *ctx);
 int mm_version(void);
+/* sha256 prefix (16 hex digits) of the sources this library was built from
+   (mastering_amd/srcsha.py: the csrc sources and this header) */
+const char *mm_source_sha(void);
 
 /* ---- whole chain -------------------------------------------------------- */
 /* Host buffers: in = interleaved [frames_in*channels] of job->in_kind (f32 =

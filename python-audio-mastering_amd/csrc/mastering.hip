@@ -1219,6 +1219,11 @@ extern "C" {
 
 int mm_version(void) { return 1; }
 
+#ifndef MM_SOURCE_SHA
+#define MM_SOURCE_SHA "unknown"
+#endif
+const char *mm_source_sha(void) { return MM_SOURCE_SHA; }
+
 int mm_create(int device, mm_ctx **out) {
     if (!out) return MM_ERR_ARG;
     *out = nullptr;

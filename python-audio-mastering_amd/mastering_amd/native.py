@@ -66,7 +66,8 @@ class MMWavInfo(ctypes.Structure):
 
 
 # every symbol include/mastering.h declares (checked by tests/test_abi.py)
-EXPORTS = ("mm_create", "mm_destroy", "mm_last_error", "mm_sync", "mm_version", "mm_master", "mm_master_device",
+EXPORTS = ("mm_create", "mm_destroy", "mm_last_error", "mm_sync", "mm_version", "mm_source_sha", "mm_master",
+           "mm_master_device",
            "mm_stage_chunks", "mm_kweight_range_end", "mm_hop_energies", "mm_gate_loudness", "mm_finalize",
            "mm_read_mix", "mm_timing", "mm_kernel_stats", "mm_comm_unique_id", "mm_comm_init", "mm_comm_destroy",
            "mm_allreduce_sum_f64", "mm_allgather_f64", "mm_wav_probe", "mm_master_wav",
@@ -99,6 +100,7 @@ def load():
             "mm_last_error": ([vp], ctypes.c_char_p),
             "mm_sync": ([vp], ctypes.c_int),
             "mm_version": ([], ctypes.c_int),
+            "mm_source_sha": ([], ctypes.c_char_p),
             "mm_master": ([vp, P(MMJob), vp, vp, P(MMResult)], ctypes.c_int),
             "mm_master_device": ([vp, P(MMJob), vp, vp, P(MMResult)], ctypes.c_int),
             "mm_master_batch": ([vp, ctypes.c_int, P(MMJob), P(vp), P(vp), P(MMResult)], ctypes.c_int),
@@ -201,3 +203,8 @@ def context(device: int = 0) -> Context:
     if device not in ctxs:
         ctxs[device] = Context(device)
     return ctxs[device]
+
+
+def library_sha() -> str:
+    """Source hash embedded in the loaded library (srcsha.library_sha at build time)."""
+    return load().mm_source_sha().decode()

@@ -38,6 +38,13 @@ def test_library_exports_every_declared_symbol():
     assert lib.mm_version() >= 1
 
 
+def test_library_was_built_from_these_sources():
+    """The library carries the hash of the sources it was compiled from
+    (Makefile -DMM_SOURCE_SHA): a stale build is caught here and in smoke()."""
+    from mastering_amd import native, srcsha
+    assert native.library_sha() == srcsha.library_sha()
+
+
 def test_struct_layouts_match_c(tmp_path):
     from mastering_amd import native
     prog = tmp_path / "layout.c"
