@@ -43,13 +43,27 @@ __device__ __forceinline__ float saturate(float x, const SatArgs &s) {
 
 // DF2T section (scipy sosfilt / lfilter form): y = b0 x + z0;
 // z0 = b1 x - a1 y + z1; z1 = b2 x - a2 y.  State s = (z0, z1).
+// SCIPY: scipy's _sosfilt operation order, every product and sum rounded
+// (y = b0*x + z0; z0 = (b1*x - a1*y) + z1; z1 = b2*x - a2*y; matched bit for bit
+// against scipy.signal.sosfilt on random data): the passes whose outputs are
+// quantised (AME:63, 204-206) use it, so with the same state they produce
+// scipy's bits.  Otherwise fused (the zero-state passes that only feed the
+// tiles' carry maps).
+template <bool SCIPY = false>
 __device__ __forceinline__ double df2t(double x, double &z0, double &z1, const double *c) {
-    double y = fma(c[0], x, z0);
-    double t0 = fma(c[1], x, z1);
-    double t1 = c[2] * x;
-    z0 = fma(-c[3], y, t0);
-    z1 = fma(-c[4], y, t1);
-    return y;
+    if constexpr (SCIPY) {
+        const double y = c[0] * x + z0;
+        z0 = (c[1] * x - c[3] * y) + z1;
+        z1 = c[2] * x - c[4] * y;
+        return y;
+    } else {
+        double y = fma(c[0], x, z0);
+        double t0 = fma(c[1], x, z1);
+        double t1 = c[2] * x;
+        z0 = fma(-c[3], y, t0);
+        z1 = fma(-c[4], y, t1);
+        return y;
+    }
 }
 
 // ------------------------------------------------------------------ EQ stage
@@ -159,7 +173,7 @@ __device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, doub
             if (!P2) a.xs[((int64_t)n * a.G + g0 + t) * CH + c] = x;  // pass 2 reads it back coalesced
             double y = (double)x;
 #pragma unroll
-            for (int s = 0; s < NS; ++s) y = df2t(y, z[s][0], z[s][1], sos[s]);
+            for (int s = 0; s < NS; ++s) y = df2t<P2>(y, z[s][0], z[s][1], sos[s]);
             if (P2) {
                 if (CH == 2 && a.width_on) {  // apply_stereo_width (AME:136-144), f64
                     const double o = pair_swap(y);
@@ -192,7 +206,7 @@ __device__ void eq_pass2(const EqArgs &a, int64_t g, int c, int len, double (&z)
         [&](float x) {
             double y = (double)x;
 #pragma unroll
-            for (int s = 0; s < NS; ++s) y = df2t(y, z[s][0], z[s][1], sos[s]);
+            for (int s = 0; s < NS; ++s) y = df2t<true>(y, z[s][0], z[s][1], sos[s]);
             if (CH == 2 && a.width_on) {  // apply_stereo_width (AME:136-144), f64
                 const double o = pair_swap(y);
                 const double yl = c == 0 ? y : o, yr = c == 0 ? o : y;
@@ -316,10 +330,10 @@ __device__ __forceinline__ void xo_pass(const XoArgs &a, int64_t g, int c, int l
         len, [&](int i) { return a.q_in[((int64_t)min(i, len - 1) * G + g) * 2 + c]; },
         [&](int16_t q) {
             const double x = (double)((float)q / 32768.0f);  // AME:199 int16 -> f32
-            double yl = df2t(x, z[0][0], z[0][1], sos[0]);
-            yl = df2t(yl, z[1][0], z[1][1], sos[1]);
-            double yh = df2t(x, z[2][0], z[2][1], sos[2]);
-            yh = df2t(yh, z[3][0], z[3][1], sos[3]);
+            double yl = df2t<P2>(x, z[0][0], z[0][1], sos[0]);
+            yl = df2t<P2>(yl, z[1][0], z[1][1], sos[1]);
+            double yh = df2t<P2>(x, z[2][0], z[2][1], sos[2]);
+            yh = df2t<P2>(yh, z[3][0], z[3][1], sos[3]);
             if (P2) {
                 const double ym = (x - yl) - yh;  // AME:202
                 const int64_t o = ((int64_t)pn * G + g) * 2;

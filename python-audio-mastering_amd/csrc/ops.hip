@@ -190,7 +190,7 @@ __device__ __forceinline__ void iir_op_pass(const IirOpArgs &a, int64_t g, int c
             double y = x;
 #pragma unroll
             for (int s = 0; s < NS; ++s) {
-                y = df2t(y, z[s][0], z[s][1], a.sos[s]);
+                y = df2t<P2>(y, z[s][0], z[s][1], a.sos[s]);
                 if (R32) y = (double)(float)y;
             }
             if (P2) {

@@ -21,3 +21,20 @@ def oracle():
     from oracle import mastering_oracle as mo
     mo.build()
     return mo
+
+
+# identical-sample fractions of the GPU parity tests (printed at the end of the run,
+# so the -q output of `pytest -m gpu` carries every test's measured exactness)
+EXACTNESS = []
+
+
+def record_exact(value, what="out"):
+    test = os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0]
+    EXACTNESS.append((test, what, float(value)))
+
+
+def pytest_terminal_summary(terminalreporter):
+    if EXACTNESS:
+        terminalreporter.write_sep("-", "identical-sample fractions (GPU vs oracle / reference fixtures)")
+        for test, what, v in EXACTNESS:
+            terminalreporter.write_line(f"exact {v:.7f} {what:5s} {test}")

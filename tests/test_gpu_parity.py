@@ -8,7 +8,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN
+from conftest import GOLDEN, record_exact
 
 pytestmark = pytest.mark.gpu
 
@@ -24,10 +24,24 @@ def rms_diff(a, b):
     return float(np.sqrt(np.mean(((a.astype(np.float64) - b.astype(np.float64)) / 32768.0) ** 2)))
 
 
-def _check(out, info, ref, L):
+# Identical int16 output samples, tied to what is measured (round 3, `pytest -m gpu`
+# summary): 99.960-99.992 % on every full-chain case but loud_sat100 (99.871 %).  The
+# differences come from numpy's float32 tanh (not correctly rounded),
+# carried through the compressor; with the exciter off the pre-gain mix is 100 %
+# identical (test_mix_bit_exact_without_tanh).  The floor allows twice the worst
+# measured mismatch rate, so a regression from 99.98 % to 99.9 % fails.
+MIN_EXACT = 0.9992
+
+
+def _check(out, info, ref, L, min_exact=MIN_EXACT):
+    """North-star tolerances, plus the identical-sample floor; records the
+    fraction (printed at the end of the run)."""
     assert out.shape == ref.shape
     r = rms_diff(out, ref)
     exact = float(np.mean(out == ref))
+    record_exact(exact)
+    if min_exact is not None:
+        assert exact >= min_exact, f"identical-sample fraction {exact:.7f} < {min_exact}"
     assert r <= RMS_TOL, f"rms diff {r:.3e} (exact frac {exact:.6f})"
     if L is not None and np.isfinite(L):
         assert abs(info["loudness"] - L) <= LU_TOL
@@ -46,7 +60,9 @@ def test_golden(path):
     st = json.loads(str(d["settings"]))
     out, info = master_pcm(d["pcm"], int(d["rate"]), st)
     L = float(d["loudness"])
-    _check(out, info, d["out"], None if np.isnan(L) else L)
+    # saturation 100 %: the exciter's tanh decides every sample (measured 99.871 %)
+    floor = 0.997 if os.path.basename(path) == "loud_sat100.npz" else MIN_EXACT
+    _check(out, info, d["out"], None if np.isnan(L) else L, floor)
 
 
 @pytest.mark.parametrize("seconds,params,track", [(35, P_FULL, 1), (12, P_HOT, 2)])
@@ -86,13 +102,17 @@ def _oracle_mix(oracle, pcm, params):
 
 def test_mix_bit_exact_without_tanh(oracle):
     """Pre-gain mix (chunks + EQ + width + multiband + overlay, AME:48-80) with the
-    exciter off: everything left is f64 IIR (tile-scan carries differ from scipy in the
-    last bits only) and integer work, so >= 99.9999 % of samples must be identical."""
+    exciter off: the quantised IIR passes run scipy's own operation order (iir.hip
+    df2t<true>), the rest is integer work and the exact envelope solve, so the int16
+    mix is identical to the oracle's (measured 100 %; only a tile-scan carry that
+    differs from scipy's serial state in its last bit next to an int16 boundary could
+    move a sample)."""
     from mastering_amd.synth import pink_noise_pcm16
     params = dict(P_HOT, saturation=0)
     pcm = pink_noise_pcm16(31 * 44100, 44100, 2, 5)
     mix, ref = _staged_mix(pcm, params), _oracle_mix(oracle, pcm, params)
-    assert np.mean(mix == ref) >= 0.999999, np.mean(mix == ref)
+    record_exact(np.mean(mix == ref), "mix")
+    assert np.array_equal(mix, ref), np.mean(mix == ref)
 
 
 def test_mix_with_exciter(oracle):
@@ -101,7 +121,8 @@ def test_mix_with_exciter(oracle):
     from mastering_amd.synth import pink_noise_pcm16
     pcm = pink_noise_pcm16(31 * 44100, 44100, 2, 5)
     mix, ref = _staged_mix(pcm, P_HOT), _oracle_mix(oracle, pcm, P_HOT)
-    assert rms_diff(mix, ref) <= RMS_TOL and np.mean(mix == ref) >= 0.999
+    record_exact(np.mean(mix == ref), "mix")
+    assert rms_diff(mix, ref) <= RMS_TOL and np.mean(mix == ref) >= 0.9998  # measured 99.989 %
 
 
 class _ThreadCollectives:
