@@ -332,7 +332,11 @@ __device__ __forceinline__ double lean_step(double att, double m, double inc, do
 #define MM_WALK_WB 40
 #endif
 constexpr int WALK_WB = MM_WALK_WB;  // M values in flight per walker (a multiple of CK_Q)
-constexpr int WALK_PAD = WALK_WB;  // padding rows after the compacted array (prefetch past a super-tile's end)
+#ifndef MM_P0_WB
+#define MM_P0_WB 40
+#endif
+constexpr int P0_WB = MM_P0_WB;     // the same for pass 0's walkers (latency of a lockstep wave's loads)
+constexpr int WALK_PAD = WALK_WB > P0_WB ? WALK_WB : P0_WB;  // padding rows after the compacted array (prefetch past a super-tile's end)
 constexpr int CK_Q = 10;     // checkpoint stride (compacted frames); divides WALK_WB and SEG
 // Release jumps: a super-tile is cut into segments of SEG compacted
 // frames; for each, pass 0 records the exact effect of SEG release steps on any
@@ -388,10 +392,10 @@ struct ColWalk<true> {
     }
 };
 
-template <bool CK, bool BUF = false>
+template <bool CK, bool BUF = false, int WB = WALK_WB>
 __device__ __forceinline__ double comp_walk(double att, const CompArgs &a, int b, int64_t s, int len,
                                             const BandStep &bs, int row0 = 0) {
-    constexpr int WB = WALK_WB, WP = 4;
+    constexpr int WP = 4;
     if (len <= 0) return att;
     // column s from row row0 (a multiple of CK_Q), rows RS apart; loads run up to WB
     // rows past the end (padding rows)
@@ -719,12 +723,12 @@ __global__ void __launch_bounds__(2 * PASS0_BLOCK) comp_pass0_kernel(CompArgs a)
             const int64_t k = st.p0 / a.U;  // index of s within its chunk
             const int64_t w0 = s - min((int64_t)a.warmup, k);
             att = a.Mc[b][cm_col(a, w0)];  // row 0 of super-tile w0
-            for (int64_t w = w0; w < s; ++w) att = comp_walk<false>(att, a, b, w, a.U, bs);
+            for (int64_t w = w0; w < s; ++w) att = comp_walk<false, false, P0_WB>(att, a, b, w, a.U, bs);
         } else if (!warm) {
             att = a.Mc[b][cm_col(a, s)];  // the M of its first frame
         }
         a.start[b][s] = att;
-        att = comp_walk<true>(att, a, b, s, st.len, bs);
+        att = comp_walk<true, false, P0_WB>(att, a, b, s, st.len, bs);
         a.end[b][s] = att;
         warm = true;
     }

@@ -317,7 +317,7 @@ static int launch_eq(mm_ctx *c, int nsec, int ch, unsigned nblk, const EqArgs &e
 // successor may be stale) and exits at once if sweep k-1 flagged nothing.
 // Convergence is checked at the chain's single sync (evaluate_chain); a rare
 // unconverged batch is extended there (MM_COMP_SWEEPS sets the queued count).
-constexpr int COMP_SWEEPS = 4;  // queued per chain (a sweep after a quiet one exits at once)
+constexpr int COMP_SWEEPS = 6;  // queued per chain (a sweep after a quiet one exits at once; P_HOT on C2 needs 4-5)
 
 static int comp_sweeps(mm_ctx *c, int n) {
     CompArgs &ca = c->ca;

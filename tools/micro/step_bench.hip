@@ -21,12 +21,12 @@ __device__ __forceinline__ double step(double att, double M, double inc, double 
     }
 }
 template <int V, int CHAINS>
-__global__ void bench(const double* in, int n, double* out, long long* cyc) {
-    if (threadIdx.x != 0) return;
+__global__ void bench(const double* in, int n, double* out, long long* cyc, int act) {
+    if ((int)threadIdx.x >= act) return;
     double att[CHAINS];
     for (int c = 0; c < CHAINS; ++c) att[c] = 0.1 * c;
     double M[4], inc[4], dec[4];
-    for (int k = 0; k < 4; ++k) { M[k] = in[k]; inc[k] = div_cr(M[k], 441.0, 1.0/441.0); dec[k] = div_cr(M[k], 8820.0, 1.0/8820.0); }
+    for (int k = 0; k < 4; ++k) { M[k] = in[k] + 1e-3 * threadIdx.x; inc[k] = div_cr(M[k], 441.0, 1.0/441.0); dec[k] = div_cr(M[k], 8820.0, 1.0/8820.0); }
     long long t0 = clock64();
     for (int i = 0; i < n; i += 4) {
 #pragma unroll
@@ -36,14 +36,14 @@ __global__ void bench(const double* in, int n, double* out, long long* cyc) {
     }
     long long t1 = clock64();
     double s = 0; for (int c = 0; c < CHAINS; ++c) s += att[c];
-    out[0] = s; cyc[0] = t1 - t0;
+    out[threadIdx.x] = s; if (threadIdx.x == 0) cyc[0] = t1 - t0;
 }
 template <int CHAINS>
-__global__ void bench_div(const double* in, int n, double* out, long long* cyc) {
-    if (threadIdx.x != 0) return;
+__global__ void bench_div(const double* in, int n, double* out, long long* cyc, int act) {
+    if ((int)threadIdx.x >= act) return;
     double att[CHAINS];
     for (int c = 0; c < CHAINS; ++c) att[c] = 0.1 * c;
-    double M[4]; for (int k = 0; k < 4; ++k) M[k] = in[k];
+    double M[4]; for (int k = 0; k < 4; ++k) M[k] = in[k] + 1e-3 * threadIdx.x;
     long long t0 = clock64();
     for (int i = 0; i < n; i += 4) {
 #pragma unroll
@@ -55,20 +55,22 @@ __global__ void bench_div(const double* in, int n, double* out, long long* cyc) 
     }
     long long t1 = clock64();
     double s = 0; for (int c = 0; c < CHAINS; ++c) s += att[c];
-    out[0] = s; cyc[0] = t1 - t0;
+    out[threadIdx.x] = s; if (threadIdx.x == 0) cyc[0] = t1 - t0;
 }
 template <class K>
 void run(const char* name, K k, const double* d, double* o, long long* c, int n, int chains) {
-    long long cy;
-    hipLaunchKernelGGL(k, 1, 64, 0, 0, d, n, o, c); hipDeviceSynchronize();
-    hipLaunchKernelGGL(k, 1, 64, 0, 0, d, n, o, c); hipDeviceSynchronize();
-    hipMemcpy(&cy, c, 8, hipMemcpyDeviceToHost);
-    printf("%-28s chains=%d  %.1f cycles/step/chain\n", name, chains, (double)cy / n / chains);
+    for (int act : {1, 64}) {
+        long long cy;
+        hipLaunchKernelGGL(k, 1, 64, 0, 0, d, n, o, c, act); hipDeviceSynchronize();
+        hipLaunchKernelGGL(k, 1, 64, 0, 0, d, n, o, c, act); hipDeviceSynchronize();
+        hipMemcpy(&cy, c, 8, hipMemcpyDeviceToHost);
+        printf("%-28s lanes=%2d chains=%d  %.1f cycles/step/chain\n", name, act, chains, (double)cy / n / chains);
+    }
 }
 int main() {
     double h[4] = {9.5, 9.6, 9.4, 9.55};
     double *d, *o; long long *c;
-    hipMalloc(&d, 32); hipMalloc(&o, 8); hipMalloc(&c, 8);
+    hipMalloc(&d, 32); hipMalloc(&o, 64 * 8); hipMalloc(&c, 8);
     hipMemcpy(d, h, 32, hipMemcpyHostToDevice);
     const int n = 200000;
     run("div_cr inline + minmax", bench_div<1>, d, o, c, n, 1);
