@@ -14,6 +14,9 @@ the rank's share once, inputs and outputs resident in HBM):
       all-reduce of the 0.1 s loudness energies run through the library's own RCCL
       communicator (mm_comm_init; RCCL over xGMI), "scaling": "strong".
   C5  16 x 3-min 96 kHz f32 tracks per GPU (128 over 8 GPUs), f32 out, batched.
+  C1  one 30 s 44.1 kHz track, EQ + LUFS only (pop preset; no exciter, no
+      multiband, width 1.0): BASELINE's CPU-path config, timed here on the GPU with
+      the reference's CPU path (faithful-cost leg) beside it.
 Full chain settings P_FULL (exciter 30 %, techno EQ, width 1.3, 3-band compressor
 with the worker's default thresholds, LUFS -14); `--params hot` switches to the
 P_HOT thresholds (every compressor branch fires: the envelope solve's worst case
@@ -62,7 +65,15 @@ CHAIN_BYTES_PER_FRAME = 16  # f32 L,R in + f32 L,R out
 P_FULL = {"bass_boost": 4.0, "mid_cut": 3.0, "presence_boost": 1.0, "treble_boost": 3.0,
           "saturation": 30, "width": 1.3, "multiband": True, "lufs": -14.0}
 P_HOT = dict(P_FULL, low_thresh=-16.0, mid_thresh=-21.0, high_thresh=-27.0)
+P_EQLUFS = {"bass_boost": 2.0, "mid_cut": 0.0, "presence_boost": 3.5, "treble_boost": 2.5,  # pop (AME:15-20)
+            "saturation": 0, "width": 1.0, "multiband": False, "lufs": -14.0}
+PARAMS = {"full": P_FULL, "hot": P_HOT, "eqlufs": P_EQLUFS}
+PARAMS_DESC = {"full": "full chain (sat 30, techno EQ, width 1.3, multiband defaults, LUFS -14)",
+               "hot": "full chain P_HOT thresholds", "eqlufs": "EQ + LUFS only (pop preset, LUFS -14)"}
+VALU_PEAK_G = 256 * 4 * 2.4e9 / 4 / 1e9  # G wave64 VALU instr/s: 1024 SIMDs x 2.4 GHz / 4 cycles (f64 FMA rate)
 WORKLOADS = {
+    "C1": {"rate": 44100, "seconds": 30, "tracks": 1, "params": "eqlufs",
+           "desc": "C1: one 30 s 44.1 kHz stereo f32 track"},
     "C2": {"rate": 44100, "seconds": 300, "tracks": 1, "desc": "C2: 5-min 44.1 kHz stereo f32 track per GPU"},
     "C3": {"rate": 44100, "seconds": 180, "tracks": 8, "desc": "C3: 8 x 3-min 44.1 kHz stereo f32 tracks per GPU "
                                                              "(64 over 8 GPUs), file-sharded, batched"},
@@ -118,17 +129,21 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="C2")
-    ap.add_argument("--params", choices=("full", "hot"), default="full")
+    ap.add_argument("--params", choices=sorted(PARAMS), default=None,
+                    help="settings (default: the workload's own: eqlufs for C1, else full)")
     ap.add_argument("--profile-steps", type=int, default=5, help="steps of the per-kernel event-timed pass")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-chunks", type=int, default=2, help="whole chunks timed on one core (faithful-cost leg)")
-    ap.add_argument("--cpu-procs", type=int, default=0, help="worker processes of the N-core leg (0: the box's "
-                                                              "cores, at most 16)")
+    ap.add_argument("--cpu-procs", type=int, default=0, help="worker processes of the N-core leg (0: the CPU "
+                                                              "share the job was given: MAX_JOBS when set, else "
+                                                              "every CPU of the process's affinity)")
     ap.add_argument("--profile-tag", default=None, help="profiles/<tag>_pmc_summary.json for traffic/limiter")
     ap.add_argument("--tune", action="append", default=[], metavar="NAME=INT",
                     help="tuning experiments only: set engine.NAME (COMP_WARMUP, COMP_SUPER_FRAMES) or "
                          "design.DEFAULT_TILE before the jobs are planned")
     args = ap.parse_args()
+    if args.params is None:
+        args.params = WORKLOADS[args.workload].get("params", "full")
     for kv in args.tune:
         name, val = kv.split("=")
         from mastering_amd import design, engine
@@ -144,25 +159,47 @@ def cpu_baseline(args, wl, params):
     """Faithful-cost CPU path (oracle/faithful_cost.py), 1 core and N cores."""
     from mastering_amd.synth import pink_noise_pcm16
     from oracle import faithful_cost
+    from oracle import mastering_oracle as mo
     rate = wl["rate"]
     frames = int(wl["seconds"] * rate)
     pcm = pink_noise_pcm16(frames if wl["seconds"] <= 300 else 300 * rate, rate, 2, track=0)
-    procs = args.cpu_procs or min(16, len(os.sched_getaffinity(0)))
+    affinity = len(os.sched_getaffinity(0))
+    share = os.environ.get("MAX_JOBS")
+    procs = args.cpu_procs or (int(share) if share and share.isdigit() and int(share) > 0 else affinity)
+    n_chunks = len(mo.chunk_ranges(pcm.shape[0], rate))
+    if n_chunks == 1:
+        procs = 1  # one chunk: nothing to spread over cores
     r = faithful_cost.time_track(pcm, rate, params, chunks_1core=args.cpu_chunks, procs=procs)
+    reps = 1
+    while r["track_s_1core"] * reps < 2.0 and reps < 50:  # short tracks (C1): best of repeats, >= 2 s of CPU work
+        r2 = faithful_cost.time_track(pcm, rate, params, chunks_1core=args.cpu_chunks, procs=1)
+        for k in ("per_chunk_s_1core", "tail_s"):
+            r[k] = min(r[k], r2[k])
+        reps += 1
     scale = frames / pcm.shape[0]  # C4: a 5-min sample track, chunk cost extrapolated to the 2-h track
     t1 = (r["per_chunk_s_1core"] * r["chunks"] + r["tail_s"]) * scale
-    tn = r.get("track_s_ncore", r["track_s_1core"]) * scale
-    tracks = wl["tracks"]
-    return {"value": tracks * frames / (tn * tracks), "unit": "stereo frames/s", "cores": r.get("procs", 1),
+    tn = r.get("track_s_ncore", t1) * scale
+    best = min(t1, tn)
+    stages = ("numpy/scipy stages + pydub's per-frame Python compressor loop, pyloudnorm restated"
+              if params.get("multiband") else "numpy/scipy stages, pyloudnorm restated; no multiband stage")
+    ncore = (f" and {r['procs']} chunks on {r['procs']} cores at once ({r['wall_s_per_round']:.2f} s)"
+             if r.get("procs", 1) > 1 else "")
+    return {"value": frames / best, "unit": "stereo frames/s", "cores": r.get("procs", 1) if tn <= t1 else 1,
             "kind": "port",
-            "sample": (f"faithful-cost reference path (numpy/scipy stages + pydub's per-frame Python compressor "
-                       f"loop, pyloudnorm restated): {r['sampled_chunks_1core']} whole 30 s chunks on 1 core "
-                       f"({r['per_chunk_s_1core']:.2f} s each) and {r.get('procs', 1)} chunks on "
-                       f"{r.get('procs', 1)} cores at once ({r.get('wall_s_per_round', 0):.2f} s), the whole-track "
-                       f"tail ({r['tail_s']:.2f} s), extrapolated to the {wl['desc'].split(':')[0]} track "
-                       f"({frames} frames, {r['chunks'] * scale:.0f} chunks)"),
+            "sample": (f"faithful-cost reference path ({stages}): {r['sampled_chunks_1core']} whole 30 s chunk(s) "
+                       f"on 1 core ({r['per_chunk_s_1core']:.3f} s each, best of {reps}){ncore}, the whole-track "
+                       f"tail ({r['tail_s']:.3f} s), extrapolated to the {wl['desc'].split(':')[0]} track "
+                       f"({frames} frames, {r['chunks'] * scale:.0f} chunks); value = the faster of the 1-core and "
+                       f"N-core legs"),
             "single_core": {"value": frames / t1, "cores": 1, "track_s": t1},
-            "multi_core_track_s": tn, "extrapolated": True}
+            "multi_core": ({"value": frames / tn, "cores": r["procs"], "track_s": tn} if r.get("procs", 1) > 1
+                           else None),
+            "extrapolated": r["chunks"] * scale > r["sampled_chunks_1core"],
+            "host_cpus": {"os_cpu_count": os.cpu_count(), "affinity": affinity, "max_jobs_env": share,
+                          "leg_processes": r.get("procs", 1),
+                          "policy": ("one chunk: 1 process" if n_chunks == 1 else "--cpu-procs" if args.cpu_procs
+                                     else "MAX_JOBS (the CPU share the GPU box gives one GPU's job)"
+                                     if procs != affinity else "every CPU of the affinity mask")}}
 
 
 class stdout_to_stderr:
@@ -253,6 +290,31 @@ class Runner:
                 self.results = r
 
 
+def valu_ceiling(prof, dom):
+    """The f64-VALU ceiling beside the HBM one, from the profile's SQ pass:
+    SQ_INSTS_VALU (wave64 VALU instructions per launch, chip total) over the
+    kernel's average duration, against 1024 SIMDs issuing one wave64 f64 FMA
+    every 4 cycles at 2.4 GHz (MI355X_MICROARCH.md: 78.6 TF f64 vector)."""
+    ks = prof.get("kernels", {})
+
+    def one(k):
+        q = ks.get(k, {})
+        n, ns = (q.get("sq") or {}).get("SQ_INSTS_VALU"), q.get("avg_ns")
+        if not n or not ns:
+            return None
+        g = n / (ns * 1e-9) / 1e9
+        return {"achieved": g, "frac": g / VALU_PEAK_G, "instrs_per_launch": n, "avg_launch_ms": ns / 1e6}
+
+    per = {k: one(k) for k in ks}
+    per = {k: v for k, v in per.items() if v}
+    tot_ns = sum(ks[k]["avg_ns"] * ks[k].get("launches_per_step", 1) for k in per)
+    chain = (sum(v["frac"] * ks[k]["avg_ns"] * ks[k].get("launches_per_step", 1) for k, v in per.items()) / tot_ns
+             if tot_ns else None)
+    return {"unit": "G wave64 VALU instr/s", "peak": VALU_PEAK_G, "dominant_kernel": per.get(dom),
+            "chain_time_weighted_frac": chain,
+            "per_kernel_frac": {k: round(v["frac"], 4) for k, v in per.items()}}
+
+
 def profile_summary(tag):
     path = os.path.join(ROOT, "profiles", f"{tag}_pmc_summary.json")
     try:
@@ -268,7 +330,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     wl = WORKLOADS[args.workload]
-    params = P_HOT if args.params == "hot" else P_FULL
+    params = PARAMS[args.params]
 
     # the CPU baseline first: its worker processes fork before anything initialises the GPU
     cpu = None
@@ -338,9 +400,11 @@ def main():
         chain_gbs = CHAIN_BYTES_PER_FRAME * n_frames / (ms_step / 1e3) / 1e9
         # PMC traffic and SQ shares, only from a profile of these exact sources
         sha = source_sha()
-        tag = args.profile_tag or f"r02_{args.workload}" + ("hot" if args.params == "hot" else "")
+        default_params = WORKLOADS[args.workload].get("params", "full")
+        tag = args.profile_tag or f"r03_{args.workload}" + ("" if args.params == default_params else args.params)
         prof, prof_path = profile_summary(tag)
         traffic = limiter = dom_traffic = None
+        valu = None
         prof_note = f"no profile at {os.path.relpath(prof_path, ROOT)}"
         if prof is not None:
             if prof.get("source_sha") != sha:
@@ -352,14 +416,13 @@ def main():
                 limiter = prof.get("chain", {}).get("limiter")
                 k = prof.get("kernels", {}).get(dom, {})
                 dom_traffic = k.get("bytes_per_launch")
+                valu = valu_ceiling(prof, dom)
         line = {
             "metric": METRIC, "value": value, "unit": "stereo frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
             "scaling": "strong" if args.workload == "C4" else "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": wl["desc"] + (", full chain P_HOT thresholds" if args.params == "hot" else
-                                                 ", full chain (sat 30, techno EQ, width 1.3, multiband defaults, "
-                                                 "LUFS -14)"),
+            "config": {"workload": wl["desc"] + ", " + PARAMS_DESC[args.params],
                        "frames_per_track": int(wl["seconds"] * wl["rate"]), "tracks_per_gpu": wl["tracks"],
                        "rate": wl["rate"], "frames_per_rank_step": n_frames,
                        "parallelism": (f"time-sharded x{world} (library RCCL)" if args.workload == "C4"
@@ -373,7 +436,8 @@ def main():
                          "dominant_kernel": {"name": dom, "achieved": k_achieved,
                                              "frac": k_achieved / HBM_PEAK_GBS if k_achieved else None,
                                              "algorithmic_bytes_per_launch": bpl, "avg_launch_ms": avg_s * 1e3,
-                                             "launches_per_step": launches, "traffic": dom_traffic}},
+                                             "launches_per_step": launches, "traffic": dom_traffic},
+                         "valu_ceiling": valu},
             "chain": {"device_ms_per_step": sum(v[0] for v in per.values()),
                       "comp_iters": iters, "comp_active_frames": active, "comp_rewalked_frames": walked, "comp_jumped_frames": jumped,
                       "kernels_ms_per_step": {k: round(v[0], 4) for k, v in per.items()}},

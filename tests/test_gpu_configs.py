@@ -10,6 +10,7 @@ against the CPU oracle (tolerances as test_gpu_parity.py: north_star PCM RMS
       against the oracle on the whole track;
   C5  a 3-min 96 kHz track fed as a 32-bit float WAV through process(), and a
       batch of 16 such tracks through mm_master_batch (f32 out);
+  C1  a 30 s 44.1 kHz WAV through process() with EQ + LUFS only (pop preset);
 plus the compressor's worst case: a 5-min P_HOT track (every envelope branch
 fires), with its sweep count and re-walked frames bounded."""
 import threading
@@ -25,6 +26,23 @@ pytestmark = pytest.mark.gpu
 def _oracle_check(oracle, out, info, pcm, rate, params):
     ref, L = oracle.master(pcm, rate, params, return_loudness=True)
     return _check(out, info, ref, L)
+
+
+@pytest.mark.timeout(300)
+def test_c1_eq_lufs_30s_wav(tmp_path, oracle):
+    """C1 (BASELINE configs[0]): 30 s 44.1 kHz stereo WAV, EQ + LUFS only, pop
+    preset, WAV in -> WAV out through the worker's process() entry point."""
+    import bench
+    from mastering_amd import process, wavio
+    from mastering_amd.synth import pink_noise_pcm16
+    rate = 44100
+    pcm = pink_noise_pcm16(30 * rate, rate, 2, 600)
+    src, dst = tmp_path / "in.wav", tmp_path / "out.wav"
+    wavio.write_wav(str(src), pcm, rate)
+    info = process(str(src), str(dst), dict(bench.P_EQLUFS))
+    got, r = wavio.read_wav(str(dst))
+    assert r == rate and got.dtype == np.int16 and got.shape == pcm.shape
+    _oracle_check(oracle, got, info, pcm, rate, bench.P_EQLUFS)
 
 
 @pytest.mark.timeout(900)

@@ -2,7 +2,9 @@
 kernel-trace stats CSV) for bench.py's `traffic` / `limiter` fields.
 
 Per kernel: launches per step, average duration (kernel trace), FETCH_SIZE /
-WRITE_SIZE bytes per launch, SQ issue/wait shares and the limiter they point at.
+WRITE_SIZE bytes per launch, SQ issue/wait shares and the limiter they point at, and `valu_frac`:
+SQ_INSTS_VALU per launch over the duration against the chip's f64-VALU issue
+ceiling (1024 SIMDs x one wave64 instruction per 4 cycles at 2.4 GHz).
 Per step ("chain"): bytes = sum over kernels of bytes per launch x launches per
 step.  `source_sha` (bench.source_sha) ties the file to the kernel sources it
 measured: bench.py ignores a profile of other sources.
@@ -27,6 +29,7 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 HBM_PEAK = 8.0e12
+VALU_PEAK = 256 * 4 * 2.4e9 / 4  # wave64 VALU instr/s: 1024 SIMDs, one f64 FMA per 4 cycles at 2.4 GHz
 
 
 def label(name):
@@ -93,9 +96,11 @@ def main():
         util = bpl / (avg_ns * 1e-9) / HBM_PEAK if avg_ns else None
         q = {c: sum(v) / len(v) for c, v in sq.get(k, {}).items() if v}
         lim, shares = limiter(q, util)
+        vi = q.get("SQ_INSTS_VALU")
+        valu_frac = vi / (avg_ns * 1e-9) / VALU_PEAK if vi and avg_ns else None
         out["kernels"][k] = {"launches_per_step": launches, "avg_ns": avg_ns, "fetch_raw": fb, "write": wb,
                              "bytes_per_launch": bpl, "bytes_per_launch_fetch_x2": 2 * (fb or 0) + (wb or 0),
-                             "hbm_util": util, "limiter": lim, "sq_shares": shares, "sq": q}
+                             "hbm_util": util, "valu_frac": valu_frac, "limiter": lim, "sq_shares": shares, "sq": q}
         chain_b += bpl * launches
         chain_b2 += (2 * (fb or 0) + (wb or 0)) * launches
         if avg_ns and lim:
@@ -108,7 +113,8 @@ def main():
     with open(os.path.join(prof, f"{tag}_pmc_summary.json"), "w") as g:
         json.dump(out, g, indent=1)
     print(json.dumps({k: {"ns": v["avg_ns"], "MB": round(v["bytes_per_launch"] / 1e6, 1), "lim": v["limiter"],
-                          "valu": round(v["sq_shares"].get("valu_issue", 0), 3)} for k, v in out["kernels"].items()},
+                          "valu_issue": round(v["sq_shares"].get("valu_issue", 0), 3),
+                          "valu_frac": v["valu_frac"] and round(v["valu_frac"], 3)} for k, v in out["kernels"].items()},
                      indent=0))
     print(json.dumps(out["chain"]))
 
