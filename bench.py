@@ -108,12 +108,8 @@ def algorithmic_bytes(kernel, n, g, active, walked_per_launch):
         "pre_pointwise": 8 * n + 4 * n,
         "xover": 4 * n + 12 * n,              # q1 in; three int16-pair bands out
         "comp_rms": 12 * n + 6 * n,           # bands in; uint16 rms x3 out
-        "comp_offsets": 3 * g * 8,            # counts in, offsets out
-        "comp_compact": 6 * n + 8 * active,   # rms in; M of active frames out
-        "comp_pass0": 8 * active,             # M of every active frame
-        "comp_fix": 8 * walked_per_launch,    # M of the re-walked frames
-        "comp_record": 16 * active,           # M in, att out
-        "comp_tstart": 3 * g * 12,
+        "comp_pass0": 6 * n,                  # uint16 rms of every band-frame (the table gathers hit L2)
+        "comp_fix": 2 * walked_per_launch,    # rms of the re-walked frames
         "comp_apply": 6 * n + 12 * n + 4 * n,  # rms, bands in; mix out
         "kweight": 4 * n,                     # mix in
         "seg_reduce": g * 24,

@@ -134,8 +134,8 @@ struct SatArgs {
 struct CompArgs {
     int64_t N_proc, G;
     int T, K, ch, warmup;
-    int U;                     // active frames per super-tile (envelope solve unit)
-    int64_t SPC;               // super-tiles reserved per chunk = ceil(chunk frames / U)
+    int TPS;                   // tiles per super-tile (envelope solve unit)
+    int64_t SPC;               // super-tiles per chunk = ceil(K / TPS)
     int64_t GS;                // super-tiles = chunks * SPC
     const short2 *band[3];
     const double *lut[3];      // device tables [32769]: M per integer rms
@@ -143,36 +143,27 @@ struct CompArgs {
     int look[3];
     double attack_frames[3], release_frames[3];
     double rcp_attack[3], rcp_release[3];
-    uint16_t *r16[3];          // tile-major audioop.rms per frame
+    double *Ms[3];             // super-tile-major M plane, column blocks of 64 x RP rows (compressor.hip tile_col)
+    int RP;                    // rows per column of the M plane (TPS*T + prefetch padding)
+    uint32_t ms_bytes;         // bytes of one band's M plane (buffer descriptors: < 4 GB)
     const double *E[3], *tail[3];  // per tile: sum of L^2+R^2, and over its last look % T frames
     int32_t *cnt[3];           // per tile: active frames
-    int32_t *off[3];           // per tile: compacted index of its first active frame (in chunk)
-    int32_t *total[3];         // per chunk: active frames
-    double *Mc[3];             // compacted M of active frames, chunk blocks [chunk][U + 1 + pad][RS]
-    double *ck[3];             // envelope checkpoints: state on entry to compacted rows o = 0, Q, 2Q, ...
-                               // of every super-tile, [U / Q][GS] (written by the owning walks)
-    int own;                   // super-tiles walked per pass-0 lane (after one warm-up)
-    int64_t ocols;             // ceil(SPC / own): pass-0 lanes per chunk and band
-    int64_t RS;                // row stride of a chunk's block of Mc / ck (own * ocols >= SPC columns)
-    int64_t CB, CKB;           // elements of one chunk's block of Mc ([U + 1 + pad][RS]) and of ck
-    uint32_t mc_bytes, ck_bytes;  // bytes of one band's Mc / ck (buffer descriptors)
-    int buf_ok;                // both under 2 GB: walks use buffer loads (compressor.hip ColWalk)
+    double *mmax[3];           // per tile: largest M
+    int32_t *total[3];         // per chunk: active frames (statistics)
+    double *tst[3];            // per tile of an active super-tile: envelope state on entry (owning walks)
+    int32_t *act[3];           // per super-tile: holds an active frame
+    int32_t *prv[3], *nxt[3];  // per super-tile: previous / next active super-tile of the chunk (-1: none)
+    double *desc[3];           // per active tile: release-jump descriptor [G][2 + 2 JB] (compressor.hip SegDesc)
     double *start[3];          // per-super-tile start state
     double *end[3];            // per-super-tile end state (one buffer; sweeps hand ends over with sc1 accesses)
     uint32_t *claim[3];        // per super-tile: the last sweep stamp that claimed it (zeroed per chain)
-    int SPT;                   // jump segments per super-tile (U / SEG)
-    double *desc[3];           // release-jump descriptors [GS][SPT][2 + 2 JB] (compressor.hip SegDesc)
-    double *jstart[3];         // per segment: entry state recorded by the sweep that jumped it
-    uint32_t *jmark[3];        // per segment: chain tag of that jump (0 / older tags: none this chain)
-    uint32_t tag;              // this chain's tag (never 0)
-    uint32_t *jlist[3];        // per band: segments (t * GS + s) newly marked this chain, for comp_refill
-    uint32_t *jlist_n;         // [3] their counts (zeroed per chain; > jlist_cap: overflowed, refill scans all)
-    uint32_t jlist_cap;
     int jumps;                 // release jumps enabled (MM_COMP_NOJUMP=1 disables them: diagnostics)
     uint32_t stamp;            // this sweep's stamp (> every earlier one of the chain)
     int heads;                 // 0: Jacobi sweep (every stale super-tile walks); 1: run heads only
     unsigned int *changed;
     unsigned long long *walked;  // [0] frames re-walked, [1] frames jumped by the fix-up sweeps (statistics)
+    uint32_t *trace;           // diagnostics (MM_FIX_TRACE): per sweep, band, super-tile {10 ns ticks, walked, jumped, held, visited}
+    int sweep_idx;
     short2 *q_out;
 };
 

@@ -87,8 +87,6 @@ struct mm_ctx {
     size_t rb_cap = 0;
     // batch execution (mm_master_batch): child contexts, one stream each
     std::vector<mm_ctx *> children;
-    int concurrency = 1;  // chains running beside this one (batch streams): sizes pass-0 ownership
-    int own_override = 0;  // MM_PASS0_OWN (tuning): fixed pass-0 ownership
     // rccl
     ncclComm_t comm = nullptr;
     int rank = 0, nranks = 1;
@@ -266,6 +264,7 @@ static int validate(mm_ctx *c, const mm_job *j) {
         return set_err(c, MM_ERR_ARG, "K-weighting tables built for %d-frame tiles", j->kweight.tile);
     if (j->multiband_on) {
         if (j->xover.nsec != 4 || j->xover.nsec_branch0 != 2) return set_err(c, MM_ERR_ARG, "crossover must be 2+2 sections");
+        if (j->tile % WB != 0) return set_err(c, MM_ERR_ARG, "the envelope solve needs tiles of a multiple of %d frames", WB);
         for (int b = 0; b < 3; ++b) {
             if (!j->band[b].lut) return set_err(c, MM_ERR_ARG, "band %d: missing table", b);
             if (j->band[b].look < 0) return set_err(c, MM_ERR_ARG, "band %d: look < 0", b);
@@ -326,33 +325,27 @@ static int comp_sweeps(mm_ctx *c, int n) {
         HIPCHK(c, hipMemsetAsync(c->comp_changed, 0, 16 * sizeof(unsigned int), c->stream));
     c->comp_flags_fresh = false;
     for (int k = 0; k < n; ++k) {
+        ca.sweep_idx = (int)c->comp_stamp;
         ca.stamp = ++c->comp_stamp;
         ca.heads = ca.stamp > 1 ? 1 : 0;  // the chain's first sweep is a Jacobi step
         ca.changed = c->comp_changed + k;
         const unsigned int *prevf = k > 0 ? c->comp_changed + (k - 1) : nullptr;
-        if (ca.buf_ok) RET(launch(c, "comp_fix", comp_fix_kernel<true>, dim3(blocks_for(NS, 64), 3), dim3(64), 0, ca, prevf));
-        else RET(launch(c, "comp_fix", comp_fix_kernel<false>, dim3(blocks_for(NS, 64), 3), dim3(64), 0, ca, prevf));
+        RET(launch(c, "comp_fix", comp_fix_kernel, dim3(blocks_for(NS, 64), 3), dim3(64), 0, ca, prevf));
     }
     c->comp_pending = n;
     return MM_OK;
 }
 
-// gains + overlay into q2, every tile starting from the walkers' checkpoints
+// gains + overlay into q2, every tile starting from its stored entry state
 static int comp_back(mm_ctx *c) {
     const CompArgs &ca = c->ca;
-    // checkpoints of the segments the sweeps jumped over, then the gains
-    // grid-stride over each band's marked segments: enough lanes that a heavily
-    // jumped solve (P_HOT: tens of thousands of segments) refills in one pass
-    const dim3 gr((unsigned)std::min<int64_t>(1024, std::max<int64_t>(16, (int64_t)ca.SPT * ca.GS / 64)), 3);
-    if (ca.buf_ok) RET(launch(c, "comp_refill", comp_refill_kernel<true>, gr, dim3(64), 0, ca));
-    else RET(launch(c, "comp_refill", comp_refill_kernel<false>, gr, dim3(64), 0, ca));
     return launch(c, "comp_apply", comp_apply_kernel, dim3(blocks_for(ca.G, APPLY_TILES)), dim3(3 * APPLY_TILES), 0,
                   ca);
 }
 
 // Pinned readback block of one chain pass (offsets in bytes): look-back error
 // word, sweep flags, re-walked frame count, loudness + gain, per-chunk active counts.
-constexpr size_t RB_ERR = 0, RB_FLAGS = 16, RB_WALKED = 80, RB_LG = 96, RB_JLIST = 112, RB_TOTALS = 128;
+constexpr size_t RB_ERR = 0, RB_FLAGS = 16, RB_WALKED = 80, RB_LG = 96, RB_TOTALS = 128;
 static size_t rb_bytes(int64_t nch) { return RB_TOTALS + (size_t)12 * nch; }
 
 static int ensure_rb(mm_ctx *c, size_t bytes) {
@@ -381,11 +374,36 @@ static int queue_readback(mm_ctx *c, bool lufs) {
 // block only waits on blocks that started before it) and whether the queued
 // sweeps converged.
 static int evaluate_chain(mm_ctx *c, bool *converged) {
-    if (getenv("MM_DEBUG_JLIST"))
-        fprintf(stderr, "jlist_n=%u walked=%llu jumped=%llu\n", reinterpret_cast<const unsigned *>(c->rb + RB_JLIST)[0],
-                *reinterpret_cast<const unsigned long long *>(c->rb + RB_WALKED),
+    if (getenv("MM_DEBUG_WALKED"))
+        fprintf(stderr, "walked=%llu jumped=%llu\n", *reinterpret_cast<const unsigned long long *>(c->rb + RB_WALKED),
                 *reinterpret_cast<const unsigned long long *>(c->rb + RB_WALKED + 8));
     if (*reinterpret_cast<const unsigned *>(c->rb + RB_ERR)) return set_err(c, MM_ERR_STATE, "IIR look-back timed out");
+    if (c->comp_on && c->ca.trace) {  // MM_FIX_TRACE: the three slowest walkers of every sweep
+        const int64_t NS = c->ca.GS;
+        std::vector<uint32_t> tr((size_t)16 * 3 * NS * 5);
+        HIPCHK(c, hipMemcpy(tr.data(), c->ca.trace, tr.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        for (int k = 0; k < 16; ++k) {
+            std::vector<std::pair<uint32_t, int64_t>> v;
+            int64_t nw = 0;
+            for (int64_t i = 0; i < 3 * NS; ++i) {
+                const uint32_t *r = &tr[((size_t)k * 3 * NS + i) * 5];
+                if (r[0] || r[4]) {
+                    v.push_back({r[0], i});
+                    ++nw;
+                }
+            }
+            if (v.empty()) continue;
+            std::sort(v.rbegin(), v.rend());
+            fprintf(stderr, "sweep %d: %lld walkers;", k, (long long)nw);
+            for (size_t q = 0; q < std::min<size_t>(3, v.size()); ++q) {
+                const uint32_t *r = &tr[((size_t)k * 3 * NS + v[q].second) * 5];
+                fprintf(stderr, " [band %lld st %lld: %.1f us walked %u jumped %u held %u visited %u]",
+                        (long long)(v[q].second / NS), (long long)(v[q].second % NS), r[0] / 100.0, r[1], r[2],
+                        r[3], r[4]);
+            }
+            fprintf(stderr, "\n");
+        }
+    }
     *converged = true;
     if (c->comp_on && c->comp_pending) {
         const unsigned *flags = reinterpret_cast<const unsigned *>(c->rb + RB_FLAGS);
@@ -406,14 +424,13 @@ static int chain_check(mm_ctx *c, bool *converged) {
     return evaluate_chain(c, converged);
 }
 
-// Super-tile geometry of the envelope solve: U active frames per super-tile,
-// SPC super-tiles reserved per chunk, nch chunks.
-static void comp_geometry(const mm_job *j, int64_t G, int *U, int64_t *SPC, int64_t *nch) {
+// Super-tile geometry of the envelope solve: TPS tiles per super-tile (the job's
+// comp_super frames rounded to whole tiles), SPC super-tiles per chunk, nch chunks.
+static void comp_geometry(const mm_job *j, int64_t G, int *TPS, int64_t *SPC, int64_t *nch) {
     const int K = j->tiles_per_chunk;
-    *U = std::max(SEG, std::min(j->comp_super, FIX_MAX_U));
-    *U -= *U % SEG;  // whole jump segments (SEG is a multiple of CK_Q and WALK_WB)
+    *TPS = std::max(1, std::min((j->comp_super + j->tile / 2) / j->tile, 64));
     *nch = (G + K - 1) / K;
-    *SPC = ((int64_t)K * j->tile + *U - 1) / *U;
+    *SPC = ((int64_t)K + *TPS - 1) / *TPS;
 }
 
 // Control words of the whole chain, zeroed by ONE memset and read back by ONE
@@ -459,65 +476,48 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     ca.ch = ch;
     ca.warmup = j->comp_warmup;
     int64_t nchunks;
-    comp_geometry(j, G, &ca.U, &ca.SPC, &nchunks);
+    comp_geometry(j, G, &ca.TPS, &ca.SPC, &nchunks);
     ca.GS = nchunks * ca.SPC;
     const int64_t NS = ca.GS;
     short2 *q2;
     RET(get_buf(c, "q2", TG, &q2));
     ca.q_out = q2;
     *q2_out = q2;
-    // pass-0 ownership: one super-tile per lane without a warm-up; with one, enough
-    // lanes for the chip at C2 size (2 super-tiles per lane: the warm-up's M re-reads
-    // halve), more per lane on bigger problems and when batch streams run beside
-    // this one; MM_PASS0_OWN for experiments
-    ca.own = c->own_override > 0 ? c->own_override
-             : ca.warmup == 0   ? 1
-                                : (int)std::max<int64_t>(1, std::min<int64_t>(4, (NS * c->concurrency + 3307) / 6615));
-    ca.ocols = (ca.SPC + ca.own - 1) / ca.own;
-    ca.RS = ca.ocols * ca.own;
-    const int64_t RS = ca.RS;
-    double *st, *ends, *luts, *cks;
+    double *st, *ends, *luts, *tst, *desc, *mmax;
     uint32_t *claims;
     RET(get_buf(c, "comp_start", (size_t)3 * NS, &st));
     RET(get_buf(c, "comp_end", (size_t)3 * NS, &ends));
     claims = c->ctl_claims;  // zeroed with the control block (sized by stage_front)
-    const int64_t ck_rows = ca.U / CK_Q + WALK_WB / CK_Q;  // + rows read ahead by re-walks
-    ca.CB = RS * (ca.U + 1 + WALK_PAD);  // + compaction dummy row + walk prefetch rows
-    ca.CKB = RS * ck_rows;
-    RET(get_buf(c, "comp_ck", (size_t)3 * nchunks * ca.CKB, &cks));
     RET(get_buf(c, "comp_lut", (size_t)3 * 32769, &luts));
-    ca.SPT = ca.U / SEG;
-    const int64_t NG = (int64_t)ca.SPT * NS;  // jump segments per band
-    double *desc, *jst;
-    uint32_t *jmark;
-    RET(get_buf(c, "comp_desc", (size_t)3 * DREC * NG, &desc));
-    RET(get_buf(c, "comp_jstart", (size_t)3 * NG, &jst));
-    RET(get_buf_zeroed(c, "comp_jmark", (size_t)3 * NG, &jmark));  // tags of earlier chains never match
-    uint32_t *jlist;
-    RET(get_buf(c, "comp_jlist", (size_t)3 * NG, &jlist));
-    ca.jlist_cap = (uint32_t)std::min<int64_t>(NG, 0xffffffffll);
-    ca.jlist_n = reinterpret_cast<uint32_t *>(c->ctl + RB_JLIST);  // zeroed with the control block
-    if (++c->chain_tag == 0) ++c->chain_tag;
-    ca.tag = c->chain_tag;
+    RET(get_buf(c, "comp_tst", (size_t)3 * G, &tst));
+    RET(get_buf(c, "comp_mmax", (size_t)3 * G, &mmax));
+    RET(get_buf(c, "comp_desc", (size_t)3 * DREC * G, &desc));
     ca.jumps = getenv("MM_COMP_NOJUMP") ? 0 : 1;  // diagnostics: results must not change
     unsigned int *changed = c->comp_changed;  // zeroed with the chain's control words
     ca.walked = reinterpret_cast<unsigned long long *>(c->ctl + RB_WALKED);
-    int32_t *cnt, *off, *tot;
+    ca.trace = nullptr;
+    if (getenv("MM_FIX_TRACE")) {  // diagnostics: per-walker sweep records, printed by evaluate_chain
+        RET(get_buf(c, "comp_trace", (size_t)16 * 3 * NS * 5, &ca.trace));
+        HIPCHK(c, hipMemsetAsync(ca.trace, 0, (size_t)16 * 3 * NS * 5 * sizeof(uint32_t), c->stream));
+    }
+    ca.RP = ca.TPS * T + WALK_PAD;
+    const int64_t ms_elems = (int64_t)ca.RP * ((NS + 63) / 64) * 64;  // column blocks of 64
+    if (ms_elems * 8 >= ((int64_t)1 << 32))
+        return set_err(c, MM_ERR_ARG, "track too long for one envelope solve (%lld frames): shard it by time",
+                       (long long)j->frames_proc);
+    ca.ms_bytes = (uint32_t)(ms_elems * 8);
+    int32_t *cnt, *tot, *links;
     RET(get_buf(c, "comp_cnt", (size_t)3 * G, &cnt));
-    RET(get_buf(c, "comp_off", (size_t)3 * G, &off));
-    tot = reinterpret_cast<int32_t *>(c->ctl + RB_TOTALS);  // read back with the control block
+    RET(get_buf(c, "comp_links", (size_t)9 * NS, &links));
+    tot = reinterpret_cast<int32_t *>(c->ctl + RB_TOTALS);  // zeroed and read back with the control block
     for (int b = 0; b < 3; ++b) {
-        uint16_t *rb;
-        double *mcb;
+        double *msb;
         char nm[16];
-        snprintf(nm, sizeof nm, "comp_r%d", b);
-        RET(get_buf(c, nm, TG, &rb));
-        snprintf(nm, sizeof nm, "comp_mc%d", b);
-        RET(get_buf(c, nm, (size_t)nchunks * ca.CB, &mcb));
-        ca.r16[b] = rb;
+        snprintf(nm, sizeof nm, "comp_ms%d", b);
+        RET(get_buf(c, nm, (size_t)ms_elems, &msb));
+        ca.Ms[b] = msb;
         ca.E[b] = tile_e + (size_t)(2 * b) * G;
         ca.tail[b] = tile_e + (size_t)(2 * b + 1) * G;
-        ca.Mc[b] = mcb;
         ca.band[b] = bands[b];
         ca.lut[b] = luts + (size_t)b * 32769;
         // cached by content key (a host pointer may be reused by another table once the
@@ -536,29 +536,20 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
         ca.rcp_attack[b] = 1.0 / j->band[b].attack_frames;
         ca.rcp_release[b] = 1.0 / j->band[b].release_frames;
         ca.cnt[b] = cnt + (size_t)b * G;
-        ca.off[b] = off + (size_t)b * G;
+        ca.mmax[b] = mmax + (size_t)b * G;
         ca.total[b] = tot + (size_t)b * nchunks;
+        ca.tst[b] = tst + (size_t)b * G;
+        ca.act[b] = links + (size_t)b * NS;
+        ca.prv[b] = links + (size_t)(3 + b) * NS;
+        ca.nxt[b] = links + (size_t)(6 + b) * NS;
+        ca.desc[b] = desc + (size_t)b * DREC * G;
         ca.start[b] = st + (size_t)b * NS;
-        ca.ck[b] = cks + (size_t)b * nchunks * ca.CKB;
         ca.end[b] = ends + (size_t)b * NS;
         ca.claim[b] = claims + (size_t)b * NS;
-        ca.desc[b] = desc + (size_t)b * DREC * NG;
-        ca.jstart[b] = jst + (size_t)b * NG;
-        ca.jmark[b] = jmark + (size_t)b * NG;
-        ca.jlist[b] = jlist + (size_t)b * NG;
     }
     RET(launch(c, "comp_rms", comp_rms_kernel, dim3(nb, 3), dim3(256), 0, ca));
-    RET(launch(c, "comp_offsets", comp_offsets_kernel, dim3((unsigned)nchunks, 3), dim3(1024), 0, ca));
-    if (ca.U >= T) RET(launch(c, "comp_compact", comp_compact_kernel<true>, dim3(nb, 3), dim3(256), 0, ca));
-    else RET(launch(c, "comp_compact", comp_compact_kernel<false>, dim3(nb, 3), dim3(256), 0, ca));
-    {
-        const size_t mcb = (size_t)nchunks * ca.CB * sizeof(double), ckb = (size_t)nchunks * ca.CKB * sizeof(double);
-        ca.buf_ok = mcb < ((size_t)1 << 31) && ckb < ((size_t)1 << 31) && !getenv("MM_FLAT_WALK");
-        ca.mc_bytes = ca.buf_ok ? (uint32_t)mcb : 0u;
-        ca.ck_bytes = ca.buf_ok ? (uint32_t)ckb : 0u;
-    }
-    const dim3 g0(blocks_for(nchunks * ca.ocols, PASS0_BLOCK), 3);
-    RET(launch(c, "comp_pass0", comp_pass0_kernel, g0, dim3(2 * PASS0_BLOCK), 0, ca));
+    RET(launch(c, "comp_links", comp_links_kernel, dim3((unsigned)nchunks, 3), dim3(1024), 0, ca));
+    RET(launch(c, "comp_pass0", comp_pass0_kernel, dim3(blocks_for(NS, PASS0_BLOCK), 3), dim3(2 * PASS0_BLOCK), 0, ca));
     c->comp_on = true;
     c->ca = ca;
     c->comp_stamp = 0;
@@ -1233,7 +1224,6 @@ int mm_create(int device, mm_ctx **out) {
         delete c;
         return MM_ERR_HIP;
     }
-    if (const char *o = getenv("MM_PASS0_OWN")) c->own_override = std::max(0, std::min(8, atoi(o)));
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return MM_ERR_HIP;
@@ -1299,7 +1289,6 @@ int mm_master_batch(mm_ctx *c, int n, const mm_job *jobs, const void *const *d_i
     }
     for (int s = 0; s < S; ++s) {
         c->children[s]->timing = c->timing;
-        c->children[s]->concurrency = S;
     }
     auto enqueue = [&](mm_ctx *k, BatchUnit &u) {
         const int f = u.first;

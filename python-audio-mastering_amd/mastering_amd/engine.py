@@ -11,7 +11,6 @@ from __future__ import annotations
 
 import ctypes
 import functools
-import math
 import os
 
 import numpy as np
@@ -30,22 +29,17 @@ EQ_PRESETS = {
              "description": "Warm low-mids for guitars and punchy presence for snare/vocals."},
 }
 
-COMP_WARMUP = 6  # super-tiles of speculative warm-up walk before each one (fixed: no per-context history)
+COMP_WARMUP = 0  # super-tiles of speculative warm-up walk before each one (none: the sweeps' jumps repair starts)
 COMP_MAX_ITERS = 100000
-# envelope solve unit in active frames at 44.1 kHz.  The envelope's time constants
-# are in ms (attack/release frames scale with the rate), so the unit scales with it.
+# envelope solve unit in frames at 44.1 kHz.  The envelope's time constants are in
+# ms (attack/release frames scale with the rate), so the unit scales with it.
 COMP_SUPER_FRAMES = 1000
-COMP_SEG = 100  # release-jump segment of the envelope solve (== SEG in csrc/compressor.hip)
 
 
 def comp_super_frames(rate: int, tile: int = design.DEFAULT_TILE) -> int:
-    """Super-tile length for `rate`: whole jump segments, and whole tiles where the
-    two align (the compaction's stores stay in few lines when super-tile bounds fall
-    on tile bounds: DESIGN.md §8)."""
-    unit = COMP_SEG * tile // math.gcd(COMP_SEG, tile)
-    if unit > COMP_SUPER_FRAMES:
-        unit = COMP_SEG
-    return max(unit, int(round(COMP_SUPER_FRAMES * rate / 44100 / unit)) * unit)
+    """Super-tile length for `rate` in frames: whole tiles (the device rounds to
+    tiles; 8 x 125 at 44.1 kHz)."""
+    return max(1, int(round(COMP_SUPER_FRAMES * rate / 44100 / tile))) * tile
 
 
 class Job:

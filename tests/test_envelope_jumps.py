@@ -1,11 +1,13 @@
-"""The envelope solve's release jumps (csrc/compressor.hip comp_describe /
+"""The envelope solve's release jumps (csrc/compressor.hip Describer /
 release_jump) restated in Python and checked on the CPU: every jump
 the device would take lands bit for bit on the state pydub's step-by-step loop
 reaches (AME:207-209).
 
-The compacted M sequences come from the oracle's own band split of a pink-noise
-track at P_HOT thresholds (every envelope branch fires), so the check covers
-long release stretches, parity ties and binade crossings of real trajectories."""
+The per-frame M sequences (inactive frames M = 0 included: the solve runs in
+frame space, one descriptor per 125-frame tile) come from the oracle's own band
+split of a pink-noise track at P_HOT thresholds (every envelope branch fires), so
+the check covers long release stretches, parity ties and binade crossings of real
+trajectories."""
 import math
 import struct
 
@@ -14,7 +16,7 @@ import pytest
 
 from mastering_amd import design
 
-SEG, JB = 100, 4  # == csrc/compressor.hip
+SEG, JB = 125, 4  # tile length, binades per descriptor (== csrc/compressor.hip)
 MANT = (1 << 52) - 1
 NAN = float("nan")
 
@@ -36,8 +38,8 @@ def _step(a, m, A, R):
 
 
 def _describe(M, R):
-    """comp_describe for one segment: (max M, e0, q[2 JB])."""
-    e0 = (_bits(M[0]) >> 52) - 1023
+    """The Describer for one active tile: (max M, e0, q[2 JB]), e0 = binade of max M."""
+    e0 = (_bits(max(M)) >> 52) - 1023
     r0 = [_from(((e0 + k // 2 + 1023) << 52) | (MANT - 63 + k % 2)) for k in range(2 * JB)]
     r = list(r0)
     for m in M:
@@ -90,7 +92,7 @@ def _band_M(seconds=20):
         nz = n > 0
         rms[nz] = np.floor(np.sqrt(S[nz] / n[nz])).astype(np.int64)  # == audioop.rms (test_oracle.py)
         M = bc["table"][np.minimum(rms, 32768)]
-        out.append((M[M != 0], bc["attack_frames"], bc["release_frames"]))
+        out.append((M, bc["attack_frames"], bc["release_frames"]))
     return out
 
 
@@ -103,6 +105,8 @@ def test_release_jumps_are_exact():
             traj.append(_step(traj[-1], m, A, R))
         for s0 in range(0, len(M) - SEG + 1, SEG):
             seg = [float(v) for v in M[s0:s0 + SEG]]
+            if max(seg) == 0.0:
+                continue  # inactive tile: held, never jumped
             desc = _describe(seg, R)
             true = traj[s0]
             # the true state, its neighbours (other parity / rounding), and states in
