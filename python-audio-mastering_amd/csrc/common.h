@@ -150,10 +150,13 @@ struct CompArgs {
     int32_t *cnt[3];           // per tile: active frames
     double *mmax[3];           // per tile: largest M
     int32_t *total[3];         // per chunk: active frames (statistics)
-    double *tst[3];            // per tile of an active super-tile: envelope state on entry (owning walks)
-    int32_t *act[3];           // per super-tile: holds an active frame
-    int32_t *prv[3], *nxt[3];  // per super-tile: previous / next active super-tile of the chunk (-1: none)
-    double *desc[3];           // per active tile: release-jump descriptor [G][2 + 2 JB] (compressor.hip SegDesc)
+    int32_t *rank[3];          // per tile: active tiles before it in its chunk (comp_links)
+    int32_t *nact[3];          // per chunk: active tiles
+    // per active tile at compact index ci = chunk * K + rank:
+    int32_t *tl[3];            // the tile
+    double *mmaxc[3];          // its largest M
+    double *tstc[3];           // envelope state on entry (written by the owning walks)
+    double *descc[3];          // release-jump record [2 JB] (compressor.hip Describer)
     double *start[3];          // per-super-tile start state
     double *end[3];            // per-super-tile end state (one buffer; sweeps hand ends over with sc1 accesses)
     uint32_t *claim[3];        // per super-tile: the last sweep stamp that claimed it (zeroed per chain)

@@ -12,25 +12,28 @@
 // Markstein divisions on the device.  M == 0 exactly when rms <= thr (then att
 // is held: the step is the identity).
 //
-// The recurrence is solved EXACTLY per (chunk, band) in frame space, over
-// super-tiles of TPS consecutive tiles (1000 frames at 44.1 kHz):
-//  1. comp_rms   per (tile, band): uint16 rms per frame (tile-major, 0 past the
-//                track's end), the tile's active-frame count and largest M;
-//  2. comp_pass0 per super-tile, two waves per block:
-//                - a walker lane walks its super-tile from a guess (the M of its
-//                  first frame; exact 0 at a chunk start), storing the state on
-//                  entry to every tile (tst) and the end;
-//                - a describer lane records, per active tile, the exact effect
-//                  of the tile's T release steps on any state of the four binades
-//                  above the tile's largest M (release jumps, below);
-//  3. comp_fix   sweeps: a super-tile whose start differs from its predecessor's
-//                end re-walks from it tile by tile — held over inactive tiles,
-//                jumped over pure-release tiles, stepped otherwise — and stops as
-//                soon as its state equals the stored entry state of a tile (the
-//                stored trajectory from there on came from the same state).  At
-//                the fixed point every start is its predecessor's end: exact by
-//                induction from the chunk start;
-//  4. comp_apply per (tile, band): from the tile's stored entry state, the exact
+// The recurrence is solved EXACTLY per (chunk, band) over the chunk's ACTIVE
+// tiles (125 frames; a tile without an active frame holds the state), in
+// super-tiles of TPS consecutive active tiles (1000 frames at 44.1 kHz):
+//  1. comp_rms   per (tile, band): uint16 rms per frame, M = lut[r] gathered ONCE
+//                into a super-tile-major M plane (column blocks of 64, so 64
+//                walkers read 512 contiguous bytes per step), the tile's active
+//                count and largest M;
+//  2. comp_links per (chunk, band): ranks and lists the active tiles;
+//  3. comp_pass0 walker lanes (one per super-tile, a wave in lockstep) walk from a
+//                guess (the M of the first frame; exactly 0 at the chunk's first
+//                active tile), storing every tile's entry state and the end;
+//                describer lanes (one per active tile, on the idle SIMDs) record
+//                the exact effect of the tile's T release steps on any state of
+//                the four binades above its largest M (release jumps, below);
+//  4. comp_fix   sweeps: a super-tile whose start differs from its predecessor's
+//                end re-walks from it tile by tile — jumped over pure-release
+//                tiles, stepped otherwise — and stops as soon as its state equals
+//                a tile's stored entry state (the stored trajectory from there on
+//                came from the same state).  At the fixed point every start is
+//                its predecessor's end: exact by induction from the chunk start;
+//  5. comp_apply per (tile, band): from the tile's entry state (an inactive tile:
+//                the next active tile's, or the chunk's end), the exact
 //                trajectory, gains, audioop.mul and the overlay through LDS.
 // Pass 0 needs no warm-up: the true trajectory is in release ~90 % of the time
 // and every stretch between its clamps is crossed by jumps in the sweeps
@@ -159,10 +162,11 @@ __global__ void __launch_bounds__(256) comp_rms_kernel(CompArgs a) {
     Pair buf[NB][B];
     double mq[B];
     int pn = 0;  // rows of the pending block (its gathers in flight)
-    auto flush = [&]() __attribute__((always_inline)) {
+    // store the pending block: whole (every block but a partial last one) or its pn rows
+    auto flush = [&](bool whole) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < B; ++j)
-            if (j < pn) Mo[e + (uint32_t)j * GS32] = mq[j];
+            if (whole || j < pn) Mo[e + (uint32_t)j * GS32] = mq[j];
         e += (uint32_t)pn * GS32;
     };
     if (len > 0) {
@@ -179,10 +183,15 @@ __global__ void __launch_bounds__(256) comp_rms_kernel(CompArgs a) {
 #pragma unroll
             for (int j = 0; j < B; ++j) r[j] = j < nv ? rms_step(buf[k][j]) : 0u;
             double m[B];
+#ifdef MM_RMS_NOGATHER  // timing experiment only (wrong M)
+#pragma unroll
+            for (int j = 0; j < B; ++j) m[j] = (double)r[j];
+#else
 #pragma unroll
             for (int j = 0; j < B; ++j) m[j] = lut[r[j]];
+#endif
             __builtin_amdgcn_sched_barrier(0);
-            flush();
+            if (q > 0) flush(true);  // (the block before a block is whole)
 #pragma unroll
             for (int j = 0; j < B; ++j) buf[k][j] = ld((q + NB) * B + j);
             __builtin_amdgcn_sched_barrier(0);
@@ -204,7 +213,7 @@ __global__ void __launch_bounds__(256) comp_rms_kernel(CompArgs a) {
             for (int k = 0; k < NB; ++k)
                 if (k == nfull % NB) block(k, nfull, ntail);
         }
-        flush();
+        flush(false);
     }
     // rows past a partial last tile's frames: M = 0 (identity steps)
     for (int i = max(len, 0); i < T; ++i, e += GS32) Mo[e] = 0.0;
@@ -282,22 +291,27 @@ __device__ __forceinline__ double lean_step(double att, double m, double inc, do
 }
 
 // ---- envelope walks over the M plane ------------------------------------------
-// Super-tile s = the TPS consecutive tiles [g0, g0 + ntiles) of chunk s / SPC (the
-// chunk's last one may be shorter, or empty past the end of a short last chunk).
-// comp_links records which super-tiles hold active frames and, for each, the
-// previous and next one that does in the chunk (inactive stretches hold the state,
-// so the solve runs over active super-tiles only).
+// The solve runs over each chunk's ACTIVE tiles (an inactive tile holds the
+// state): comp_links ranks them (rank[g] = active tiles before tile g in its
+// chunk, compact index ci = chunk * K + rank), and super-tile j of chunk c is
+// the active tiles of ranks [j*TPS, min((j+1)*TPS, nact[c])) — empty past the
+// chunk's active tiles.  Its state on entry, the tiles' entry states (tstc) and
+// jump records (descc) live at compact indices.
 struct Super {
-    int64_t g0;
-    int ntiles;
+    int64_t ci0;  // compact index of its first tile
+    int ntiles;   // 0: empty
+    bool first;   // the chunk's first (starts exactly at 0)
+    bool last;    // the chunk's last non-empty one
 };
 
-__device__ __forceinline__ Super super_of(const CompArgs &a, int64_t s) {
+__device__ __forceinline__ Super super_of(const CompArgs &a, int b, int64_t s) {
     Super r;
-    const int64_t c = s / a.SPC, k = s - c * a.SPC;
-    const int64_t ce = min(c * a.K + a.K, a.G);
-    r.g0 = min(c * a.K + k * a.TPS, ce);
-    r.ntiles = (int)(min(r.g0 + a.TPS, ce) - r.g0);
+    const int64_t c = s / a.SPC, j = s - c * a.SPC;
+    const int na = a.nact[b][c];
+    r.ci0 = c * a.K + j * a.TPS;
+    r.ntiles = (int)max((int64_t)0, min((int64_t)a.TPS, (int64_t)na - j * a.TPS));
+    r.first = j == 0;
+    r.last = (j + 1) * a.TPS >= na;
     return r;
 }
 
@@ -308,50 +322,65 @@ __device__ __forceinline__ Super super_of(const CompArgs &a, int64_t s) {
 #define MM_WALK_NB 2
 #endif
 constexpr int WB = MM_WALK_B;   // rows per load block (divides T: checked on the host)
-constexpr int WNB = MM_WALK_NB; // blocks in flight
+constexpr int WNB = MM_WALK_NB; // blocks in flight (sweep walkers)
+#ifndef MM_P0_NB
+#define MM_P0_NB 2
+#endif
+constexpr int P0_NB = MM_P0_NB;  // blocks in flight (pass 0)
 constexpr int WP = 5;           // divisions run WP frames ahead of their step (divides WB)
 static_assert(WB % WP == 0, "WP must divide WB");
-constexpr int WALK_PAD = WB * WNB;  // padding rows after a column's TPS*T (prefetch)
+constexpr int WALK_PAD = WB * (WNB > P0_NB ? WNB : P0_NB);  // padding rows after a column's TPS*T (prefetch)
 
 // Buffer view of one band's M plane (byte offset of row 0 of column s: col_elem * 8)
 struct Plane {
     __amdgpu_buffer_rsrc_t r;
-    uint32_t rowb;  // bytes per row of a column block
     int RP;
 };
+constexpr uint32_t ROWB = 64u * 8u;  // bytes per row of a column block
 __device__ __forceinline__ Plane plane(const CompArgs &a, int b) {
     Plane p;
     p.r = __builtin_amdgcn_make_buffer_rsrc(a.Ms[b], (short)0, (int)a.ms_bytes, 0x00020000);
-    p.rowb = 64u * 8u;
     p.RP = a.RP;
     return p;
 }
-__device__ __forceinline__ uint32_t col_off(const Plane &p, int64_t s) {
-    return (uint32_t)(((s >> 6) * (int64_t)p.RP * 64 + (s & 63)) * 8);
+// byte offset of row 0 of tile g (its column and row k*T)
+__device__ __forceinline__ uint32_t tile_off(const CompArgs &a, int64_t g) {
+    int64_t s;
+    int k;
+    tile_col(a, g, &s, &k);
+    return (col_elem(a, s) + (uint32_t)(k * a.T) * 64u) * 8u;
 }
 __device__ __forceinline__ double ld_plane(const Plane &p, uint32_t vo, uint32_t so) {
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(p.r, vo, so, 0));
 }
 
-// Stream rows [row0, row0 + nrows) of column s (nrows a multiple of WB) to f:
-// f.tile(i) before row row0 + i*T, f.frame(j, m, m_ahead) per row (j: row in the
-// block, m_ahead: the M WP rows later).  WNB blocks in flight; no conditional
-// loads in the loop (counted waits).  LOCK: the wave's lanes step the same rows
-// (pass 0), so the row offset is an SGPR and a load costs no VALU; else per lane.
-template <bool LOCK, typename F>
-__device__ __forceinline__ void stream_col(const Plane &p, int64_t s, uint32_t row0, int nrows, int T, F &f) {
-    const int nblk = nrows / WB, bpt = T / WB;
+// Stream ntiles tiles of T rows to f, in order: f.tile(i) before tile i's first
+// row (and f.tile(ntiles) after the last), f.frame(j, m, m_ahead) per row (j: row
+// in the block, m_ahead: the M WP rows later).  offs(i) = byte offset of tile i's
+// row 0 (called once per tile, when the loads reach it).  NBK blocks in flight;
+// no conditional loads in the loop (counted waits).  LOCK: the wave's lanes step
+// the same rows (pass 0), so the row offset is an SGPR.
+template <bool LOCK, int NBK, typename OFF, typename F>
+__device__ __forceinline__ void stream_col(const Plane &p, OFF &&offs, int ntiles, int T, F &f) {
+    constexpr int WNB = NBK;
+    const int bpt = T / WB, nblk = ntiles * bpt;
     if (nblk <= 0) return;
     double mb[WNB][WB];
-    uint32_t vo = col_off(p, s) + (LOCK ? 0u : row0 * p.rowb);
-    uint32_t so = LOCK ? row0 * p.rowb : 0u;
-    const uint32_t blkb = (uint32_t)WB * p.rowb;
+    int lt = 0, lb = 0;  // load cursor: tile, block in tile
+    uint32_t vo = offs(0);
     auto load = [&](double (&d)[WB]) __attribute__((always_inline)) {
+        // LOCK: every lane is at the same row, so the row offset is one SGPR (a
+        // per-lane soffset would become a waterfall loop around every load)
+        const uint32_t rb = LOCK ? (uint32_t)__builtin_amdgcn_readfirstlane((int)((uint32_t)(lb * WB) * ROWB))
+                                 : (uint32_t)(lb * WB) * ROWB;
 #pragma unroll
         for (int j = 0; j < WB; ++j)
-            d[j] = LOCK ? ld_plane(p, vo, so + (uint32_t)j * p.rowb) : ld_plane(p, vo + (uint32_t)j * p.rowb, 0);
-        if (LOCK) so += blkb;
-        else vo += blkb;
+            d[j] = LOCK ? ld_plane(p, vo, rb + (uint32_t)j * ROWB) : ld_plane(p, vo + rb + (uint32_t)j * ROWB, 0);
+        if (++lb == bpt) {  // next tile (past the last: reload it, never consumed)
+            lb = 0;
+            if (++lt < ntiles) vo = offs(lt);
+            else lb = bpt - 1;
+        }
     };
 #pragma unroll
     for (int k = 0; k < WNB; ++k) {
@@ -384,17 +413,16 @@ __device__ __forceinline__ void stream_col(const Plane &p, int64_t s, uint32_t r
     f.tile(ct);  // (the boundary after the last row)
 }
 
-// The envelope walk as a stream consumer: with ST, the state on entry to each of
-// the first `ntiles` tiles into tst[g0 + i]; `out` = the state on entry to tile
-// `ntiles` (the end of a short super-tile walked in lockstep with full ones).
+// The envelope walk as a stream consumer: with ST, the state on entry to stream
+// tiles [i0, i0 + nst) into tst[i - i0]; `out` = the state on entry to tile
+// i0 + nst (the end of a lane's own tiles in a lockstep walk of the longest).
 template <bool ST>
 struct Walker {
-    double att, out;
+    double att, out, sv;  // sv: the state on entry to tile i0
     double inc[WP], dec[WP];
     BandStep bs;
     double *tst;
-    int64_t g0;
-    int ntiles;
+    int i0, nst;
     __device__ __forceinline__ void init(const double (&m)[WB]) {
 #pragma unroll
         for (int k = 0; k < WP; ++k) {
@@ -403,8 +431,9 @@ struct Walker {
         }
     }
     __device__ __forceinline__ void tile(int i) {
-        if (ST && i < ntiles) tst[g0 + i] = att;
-        if (i == ntiles) out = att;
+        if (ST && i >= i0 && i < i0 + nst) tst[i - i0] = att;
+        if (i == i0) sv = att;
+        if (i == i0 + nst) out = att;
     }
     __device__ __forceinline__ void frame(int j, double m, double ma) {
         const double ik = inc[j % WP], dk = dec[j % WP];
@@ -455,41 +484,16 @@ __device__ __forceinline__ bool release_jump(const SegDesc &d, double att, doubl
     return true;
 }
 
-// The describer as a stream consumer (pass 0, in lockstep with the walkers): the
-// 2 * JB reference walks of each tile, started at f.tile from the tile's largest
-// M (loaded a tile ahead) and stored at the next tile's start, off every
-// dependency chain but their own.
+// The describer of one active tile as a stream consumer: the 2 * JB reference
+// walks over its T rows, each off every dependency chain but its own.
 struct Describer {
     static constexpr uint64_t MANT = (1ull << 52) - 1;
     double r0[2 * JB], r[2 * JB];
-    double mx, mx_next;
     int e0;
     BandStep bs;
-    const double *mmax;
-    double *desc;
-    int64_t g0;
-    int ntiles, cur;
     __device__ __forceinline__ void init(const double (&)[WB]) {}
-    __device__ __forceinline__ void store() {
-        if (cur < 0 || cur >= ntiles || !(mx > 0.0)) return;  // inactive tile: held, never jumped
-        double q[2 * JB];
-#pragma unroll
-        for (int k = 0; k < 2 * JB; ++k) {
-            // the reference stayed in its binade with a nonzero mantissa (>= 2^e + u) at the end
-            const uint64_t rb = (uint64_t)__double_as_longlong(r[k]);
-            const bool ok = (rb >> 52) == (uint64_t)(e0 + k / 2 + 1023) && (rb & MANT) != 0;
-            q[k] = ok ? r0[k] - r[k] : __longlong_as_double(0x7ff8000000000000ll);
-        }
-        double2 *rec = reinterpret_cast<double2 *>(desc + (g0 + cur) * DREC);
-#pragma unroll
-        for (int k = 0; k < JB; ++k) rec[k] = make_double2(q[2 * k], q[2 * k + 1]);
-    }
     __device__ __forceinline__ void tile(int i) {
-        store();
-        cur = i;
-        mx = mx_next;
-        mx_next = mmax[g0 + max(min(i + 1, ntiles - 1), 0)];  // a tile ahead
-        e0 = mx > 0.0 ? binade(mx) : 0;
+        if (i != 0) return;
 #pragma unroll
         for (int k = 0; k < 2 * JB; ++k) {  // top of binade e0 + k/2, parity k % 2
             const uint64_t bits = ((uint64_t)(e0 + k / 2 + 1023) << 52) | (MANT - 63 + (uint64_t)(k % 2));
@@ -501,142 +505,143 @@ struct Describer {
 #pragma unroll
         for (int k = 0; k < 2 * JB; ++k) r[k] = r[k] - dec;
     }
+    __device__ __forceinline__ void store(double *rec_) const {
+        double2 *rec = reinterpret_cast<double2 *>(rec_);
+        double q[2 * JB];
+#pragma unroll
+        for (int k = 0; k < 2 * JB; ++k) {
+            // the reference stayed in its binade with a nonzero mantissa (>= 2^e + u) at the end
+            const uint64_t rb = (uint64_t)__double_as_longlong(r[k]);
+            const bool ok = (rb >> 52) == (uint64_t)(e0 + k / 2 + 1023) && (rb & MANT) != 0;
+            q[k] = ok ? r0[k] - r[k] : __longlong_as_double(0x7ff8000000000000ll);
+        }
+#pragma unroll
+        for (int k = 0; k < JB; ++k) rec[k] = make_double2(q[2 * k], q[2 * k + 1]);
+    }
 };
 
-// 2. links.  grid (chunks, 3), 1024 threads: per super-tile of the chunk whether
-// it holds an active frame (act), the previous active one (prv, -1: none, so it
-// starts at the chunk's state 0 exactly) and the next (nxt, -1: none).
+// 2. links.  grid (chunks, 3), 1024 threads: ranks the chunk's active tiles
+// (rank[g] for every tile: active tiles before it), lists them (tl[ci] = tile,
+// mmaxc[ci] = its largest M) and counts them (nact[c]).
 __global__ void __launch_bounds__(1024) comp_links_kernel(CompArgs a) {
-    __shared__ int32_t lastp[1024], firstn[1024];
+    __shared__ int32_t sums[1024];
     const int b = blockIdx.y;
-    const int64_t s0 = (int64_t)blockIdx.x * a.SPC;
-    const int n = (int)a.SPC;
+    const int64_t c = blockIdx.x, g0 = c * a.K;
+    const int n = (int)min((int64_t)a.K, a.G - g0);
     const int per = (n + 1023) / 1024;
     const int tid = threadIdx.x;
     const int i0 = min(tid * per, n), i1 = min(i0 + per, n);
-    int32_t la = -1, fa = -1;
+    int32_t cntl = 0;
+    for (int i = i0; i < i1; ++i) cntl += a.cnt[b][g0 + i] != 0 ? 1 : 0;
+    sums[tid] = cntl;
+    __syncthreads();
+    int32_t v = cntl;
+    for (int d = 1; d < 1024; d <<= 1) {
+        const int32_t o = tid >= d ? sums[tid - d] : 0;
+        __syncthreads();
+        v += o;
+        sums[tid] = v;
+        __syncthreads();
+    }
+    int32_t r = v - cntl;  // exclusive
     for (int i = i0; i < i1; ++i) {
-        const Super st = super_of(a, s0 + i);
-        int32_t v = 0;
-        for (int t = 0; t < st.ntiles; ++t) v |= a.cnt[b][st.g0 + t];
-        a.act[b][s0 + i] = v != 0 ? 1 : 0;
-        if (v != 0) {
-            la = i;
-            if (fa < 0) fa = i;
+        const int64_t g = g0 + i;
+        a.rank[b][g] = r;
+        if (a.cnt[b][g] != 0) {
+            a.tl[b][g0 + r] = (int32_t)g;
+            a.mmaxc[b][g0 + r] = a.mmax[b][g];
+            ++r;
         }
     }
-    lastp[tid] = la;
-    firstn[tid] = fa;
-    __syncthreads();
-    // inclusive max-scan of lastp (forward), min-scan of firstn (backward; -1 = none)
-    for (int d = 1; d < 1024; d <<= 1) {
-        const int32_t l = tid >= d ? lastp[tid - d] : -1;
-        const int32_t f = tid + d < 1024 ? firstn[tid + d] : -1;
-        __syncthreads();
-        if (l > lastp[tid]) lastp[tid] = l;
-        if (f >= 0 && (firstn[tid] < 0 || f < firstn[tid])) firstn[tid] = f;
-        __syncthreads();
-    }
-    int32_t prev = tid > 0 ? lastp[tid - 1] : -1;
-    for (int i = i0; i < i1; ++i) {
-        a.prv[b][s0 + i] = prev >= 0 ? (int32_t)(s0 + prev) : -1;
-        if (a.act[b][s0 + i]) prev = i;
-    }
-    int32_t next = tid < 1023 ? firstn[tid + 1] : -1;
-    for (int i = i1 - 1; i >= i0; --i) {
-        a.nxt[b][s0 + i] = next >= 0 ? (int32_t)(s0 + next) : -1;
-        if (a.act[b][s0 + i]) next = i;
-    }
+    if (tid == 1023) a.nact[b][c] = v;
 }
 
-// 3. speculative pass.  grid: (ceil(GS/64), 3), two waves per block: wave 0
-// walks, wave 1 describes the same super-tiles' tiles (it reads the same lines of
-// the M plane at the same time, from L2).  Both step the wave's 64 consecutive
-// super-tiles in lockstep over rows 0 .. TPS*T of their columns (512 contiguous
-// bytes per load).  A walker's start is exactly 0 when no active super-tile
-// precedes it in the chunk, else guessed: the M of its first frame (the state
-// tracks M), or with `warmup` > 0 found by walking that many previous columns of
-// the chunk from the M of the first warm-up frame.  Exactness never depends on
-// the guess (the fix-up sweeps).  Inactive super-tiles ride along and store
-// nothing (comp_apply gives them the previous active one's end).
-constexpr int PASS0_BLOCK = 64;
+// 3. speculative pass.  grid: (ceil(GS/64) + ceil(G/64), 3) of 64-lane blocks.
+//  * the first ceil(GS/64) blocks walk: lane = super-tile; the wave's 64 lanes
+//    step their tiles' rows in lockstep (their M-plane offsets staged in LDS).  A
+//    walker's start is exactly 0 for the chunk's first super-tile, else guessed:
+//    the M of its first frame (the state tracks M), or with `warmup` = 1 found by
+//    walking the previous super-tile from the M of its first frame.  Exactness
+//    never depends on the guess (the fix-up sweeps).
+//  * the other blocks describe: lane = tile; an active tile's release-jump record
+//    (beside the walkers on the otherwise idle SIMDs).
+constexpr int PASS0_BLOCK = 64, P0_MAXL = 64;  // lanes; tiles per walker (warm-up included)
 
-__global__ void __launch_bounds__(2 * PASS0_BLOCK) comp_pass0_kernel(CompArgs a) {
-    const bool describer = threadIdx.x >= PASS0_BLOCK;
-    const int64_t s = (int64_t)blockIdx.x * PASS0_BLOCK + (threadIdx.x % PASS0_BLOCK);
+__global__ void __launch_bounds__(PASS0_BLOCK) comp_pass0_kernel(CompArgs a, int walk_blocks) {
+    __shared__ uint32_t offs_lds[P0_MAXL][PASS0_BLOCK];
     const int b = blockIdx.y;
-    const bool live = s < a.GS && a.act[b][min(s, a.GS - 1)];
-    if (__all(!live)) return;
-    const int64_t sc = min(s, a.GS - 1);
-    const Super st = super_of(a, sc);
     const BandStep bs = band_step(a, b);
     const Plane p = plane(a, b);
-    const int rows = a.TPS * a.T;
-    if (describer) {
-        if (!a.jumps) return;
+    const int lane = threadIdx.x;
+    if ((int)blockIdx.x >= walk_blocks) {  // describer
+        const int64_t g = ((int64_t)blockIdx.x - walk_blocks) * PASS0_BLOCK + lane;
+        const bool live = g < a.G && a.cnt[b][min(g, a.G - 1)] != 0 && a.jumps;
+        if (__all(!live)) return;
+        const int64_t gc = min(g, a.G - 1);
         Describer d;
         d.bs = bs;
-        d.mmax = a.mmax[b];
-        d.desc = a.desc[b];
-        d.g0 = live ? st.g0 : 0;
-        d.ntiles = live ? st.ntiles : 0;
-        d.cur = -1;
-        d.mx = 0.0;
-        d.mx_next = a.mmax[b][d.g0];
-        stream_col<true>(p, sc, 0, rows, a.T, d);
+        const double mx = a.mmax[b][gc];
+        d.e0 = mx > 0.0 ? binade(mx) : 0;
+        const uint32_t off = tile_off(a, gc);
+        stream_col<true, P0_NB>(p, [&](int) { return off; }, 1, a.T, d);
+        if (live) d.store(a.descc[b] + ((gc / a.K) * a.K + a.rank[b][gc]) * DREC);
         return;
     }
-    const int64_t cs = (sc / a.SPC) * a.SPC;  // the chunk's first super-tile
-    const int32_t pv = a.prv[b][sc];
+    __builtin_amdgcn_s_setprio(3);  // the walkers' chains first on SIMDs they share with describers
+    const int64_t s = (int64_t)blockIdx.x * PASS0_BLOCK + lane;
+    const int64_t sc = min(s, a.GS - 1);
+    const Super st = super_of(a, b, sc);
+    const bool live = s < a.GS && st.ntiles > 0;
+    if (__all(!live)) return;
+    const int64_t cK = (sc / a.SPC) * a.K;
+    const int W = min(a.warmup, 1);
+    const int64_t cw0 = max(cK, st.ci0 - (int64_t)W * a.TPS);  // first compact index walked
+    const int nwarm = live ? (int)(st.ci0 - cw0) : 0, ntot = live ? nwarm + st.ntiles : 0;
+    int nmax = ntot;
+    for (int o = 32; o > 0; o >>= 1) nmax = max(nmax, __shfl_xor(nmax, o));
+    nmax = __builtin_amdgcn_readfirstlane(nmax);
+    const int32_t *tl = a.tl[b];
+    for (int i = 0; i < nmax; ++i)  // the walk's tile offsets (lanes past their own repeat their last)
+        offs_lds[i][lane] = tile_off(a, ntot ? tl[cw0 + min(i, ntot - 1)] : 0);
+    __syncthreads();
     double att = 0.0;
-    if (pv >= 0) {
-        const int64_t sw = max(cs, sc - (int64_t)a.warmup);
-        att = sw == cs && sw < sc ? 0.0 : ld_plane(p, col_off(p, sw), 0);  // (row 0 of column sw)
-        for (int w = a.warmup; w > 0; --w) {  // warm-up columns s - w of the chunk, lockstep
-            const int64_t cw = sc - w;
-            Walker<false> wk;
-            wk.att = att;
-            wk.out = att;
-            wk.bs = bs;
-            wk.ntiles = a.TPS;
-            stream_col<true>(p, max(cw, (int64_t)0), 0, rows, a.T, wk);
-            if (cw >= sw) att = wk.att;
-        }
-    }
+    if (live && cw0 != cK) att = ld_plane(p, offs_lds[0][lane], 0);  // the M of the walk's first frame
     Walker<true> w;
     w.att = att;
-    w.bs = bs;
-    w.tst = a.tst[b];
-    w.g0 = st.g0;
-    w.ntiles = live ? st.ntiles : 0;
     w.out = att;
-    stream_col<true>(p, sc, 0, rows, a.T, w);
+    w.sv = att;
+    w.bs = bs;
+    w.tst = a.tstc[b] + st.ci0;
+    w.i0 = nwarm;
+    w.nst = live ? st.ntiles : 0;
+    stream_col<true, P0_NB>(p, [&](int i) { return offs_lds[i][lane]; }, nmax, a.T, w);
     if (live) {
-        a.start[b][sc] = att;
-        a.end[b][sc] = w.out;
+        a.start[b][s] = w.sv;
+        a.end[b][s] = w.out;
     }
 }
 
 // 4. one fix-up sweep (exits at once if the previous sweep left nothing stale).
-// grid: (ceil(GS/64), 3), lane = super-tile; the chain of a chunk runs over its
-// active super-tiles (prv / nxt).  A lane whose start differs from its
+// grid: (ceil(GS/64), 3), lane = super-tile.  A lane whose start differs from its
 // predecessor's end CLAIMS its super-tile (atomic max of the sweep stamp: one
 // writer per super-tile per sweep) and re-walks it from that end, tile by tile:
 // coalesced (stop) when the state equals the tile's stored entry state (the
 // stored trajectory from there on, and the stored end, came from the same
-// state), else it stores the state and holds (inactive tile), jumps (exact
-// release jump) or steps through the tile.  A re-walk that reaches the end
-// without meeting the stored trajectory publishes the new end and CONTINUES into
-// the successor (whose stored trajectory started from the old end) if it can
-// claim it; if the successor's own lane claimed it first, that lane may have read
-// the old end, so the sweep flags `changed` and the next sweep re-checks.  Every
-// stale start is caught that way, so a sweep that flags nothing leaves every
-// start equal to its predecessor's end: exact by induction from the chunk start.
+// state), else it stores the state and jumps (exact release jump) or steps
+// through the tile.  A re-walk that reaches the end without meeting the stored
+// trajectory publishes the new end and CONTINUES into the successor (whose stored
+// trajectory started from the old end) if it can claim it; if the successor's own
+// lane claimed it first, that lane may have read the old end, so the sweep flags
+// `changed` and the next sweep re-checks.  Every stale start is caught that way,
+// so a sweep that flags nothing leaves every start equal to its predecessor's
+// end: exact by induction from the chunk start.
 //
-// The walker's tile sequence runs on across super-tile boundaries: the stored
-// state, largest M and jump descriptor of the tiles FIX_AHEAD positions ahead are
-// loaded while it works on the current one (into the successor's first tiles
-// near the end), so a chain of holds and jumps waits on no load.
+// A chunk's active tiles are contiguous in compact index, so the walker's
+// sequence runs on across super-tile boundaries: the stored state, largest M,
+// jump record and plane offset of the tiles FIX_AHEAD ahead are loaded while it
+// works on the current one, and a chain of jumps waits on no load.  In run-head
+// sweeps the successor is claimed on entry (a Jacobi sweep's successors belong to
+// their own lanes, so it claims at the end).
 __device__ __forceinline__ bool comp_claim(const CompArgs &a, int b, int64_t s) {
     return __hip_atomic_fetch_max((gu32 *)(a.claim[b] + s), a.stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
            a.stamp;
@@ -645,9 +650,13 @@ __device__ __forceinline__ bool comp_claim(const CompArgs &a, int b, int64_t s) 
 struct TileMeta {
     double old, mx;
     double q[2 * JB];
+    int32_t g;
 };
 
-constexpr int FIX_AHEAD = 3;
+#ifndef MM_FIX_AHEAD
+#define MM_FIX_AHEAD 3
+#endif
+constexpr int FIX_AHEAD = MM_FIX_AHEAD;
 
 // Sweep 1 (a.heads == 0) is a Jacobi step: every stale super-tile re-walks from
 // its predecessor's current end.  Later sweeps start a walker only at the HEAD of
@@ -661,49 +670,32 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
     if (prev_changed && *prev_changed == 0u) return;
     const int64_t s = (int64_t)blockIdx.x * 64 + threadIdx.x;
     const int b = blockIdx.y;
-    if (s >= a.GS || !a.act[b][s]) return;
-    const int32_t pv = a.prv[b][s];
-    if (pv < 0) return;  // the chunk's first active super-tile starts exactly at 0
+    if (s >= a.GS) return;
+    Super st = super_of(a, b, s);
+    if (st.ntiles == 0 || st.first) return;  // chunk starts are exact
     double *end = a.end[b];
-    double att = ld_sc1(end + pv);
+    double att = ld_sc1(end + s - 1);
     if (__double_as_longlong(att) == __double_as_longlong(a.start[b][s])) return;
     *a.changed = 1u;  // stale: the next sweep re-checks (benign race: every writer stores 1)
-    if (a.heads) {
-        const int32_t pp = a.prv[b][pv];
-        if (pp >= 0 && __double_as_longlong(ld_sc1(end + pp)) != __double_as_longlong(a.start[b][pv]))
-            return;  // inside a run
-    }
+    if (a.heads && (s - 1) % a.SPC != 0 &&
+        __double_as_longlong(ld_sc1(end + s - 2)) != __double_as_longlong(a.start[b][s - 1]))
+        return;  // inside a run
     if (!comp_claim(a, b, s)) return;  // a walker continuing from the predecessor owns it
     const uint64_t t_start = a.trace ? wall_clock64() : 0;
-    int n_held = 0, n_vis = 1;
+    int n_vis = 1;
     const BandStep bs = band_step(a, b);
     const Plane p = plane(a, b);
-    double *tst = a.tst[b];
-    const double *mmax = a.mmax[b];
-    const int32_t *nxt = a.nxt[b];
+    double *tst = a.tstc[b];
     const int T = a.T;
     int64_t walked = 0, jumped = 0;
-    // current super-tile and its successor in the chain (the prefetch runs into it)
-    int64_t cur = s;
-    Super st = super_of(a, cur);
-    int64_t nx = nxt[cur];
-    Super sn;  // the successor's tiles, found when the prefetch first reaches them
-    bool sn_ok = false;
-    // tile of walk position j (tile index in cur), in cur or in its successor
-    auto tile_at = [&](int j) __attribute__((always_inline)) -> int64_t {
-        if (j < st.ntiles) return st.g0 + j;
-        if (nx < 0) return st.g0 + st.ntiles - 1;
-        if (!sn_ok) {
-            sn = super_of(a, nx);
-            sn_ok = true;
-        }
-        return sn.g0 + min(j - st.ntiles, sn.ntiles - 1);
-    };
-    auto ld = [&](int64_t g) __attribute__((always_inline)) {
+    const int64_t cend = st.ci0 + (int64_t)(a.nact[b][s / a.SPC]) - (s % a.SPC) * a.TPS;  // past the chunk's last
+    auto ld = [&](int64_t ci) __attribute__((always_inline)) {
         TileMeta m;
-        m.old = tst[g];
-        m.mx = mmax[g];
-        const double2 *r = reinterpret_cast<const double2 *>(a.desc[b] + g * DREC);
+        ci = min(ci, cend - 1);
+        m.old = tst[ci];
+        m.mx = a.mmaxc[b][ci];
+        m.g = a.tl[b][ci];
+        const double2 *r = reinterpret_cast<const double2 *>(a.descc[b] + ci * DREC);
 #pragma unroll
         for (int k = 0; k < JB; ++k) {
             const double2 v = r[k];
@@ -712,58 +704,80 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
         }
         return m;
     };
+    int64_t cur = s;
+    bool nx_claimed = a.heads && !st.last ? comp_claim(a, b, cur + 1) : false;
     TileMeta ring[FIX_AHEAD];
 #pragma unroll
-    for (int k = 0; k < FIX_AHEAD; ++k) ring[k] = ld(tile_at(k));
+    for (int k = 0; k < FIX_AHEAD; ++k) ring[k] = ld(st.ci0 + k);
     a.start[b][cur] = att;
-    int i = 0;
+    int64_t ci = st.ci0, ce = st.ci0 + st.ntiles;  // position, end of cur
+    // after tile ci: the end of cur publishes its end and continues into the
+    // successor if it is (or can be) claimed; false: the walk ends
+    auto next = [&]() __attribute__((always_inline)) -> bool {
+        if (++ci < ce) return true;
+        st_sc1(end + cur, att);
+        if (st.last) return false;  // the chunk's last super-tile
+        if (!a.heads) nx_claimed = comp_claim(a, b, cur + 1);
+        if (!nx_claimed) return false;  // its owner read an older end of cur: it is stale (flagged) next sweep
+        ++cur;
+        st = super_of(a, b, cur);
+        a.start[b][cur] = att;
+        ce = st.ci0 + st.ntiles;
+        nx_claimed = a.heads && !st.last ? comp_claim(a, b, cur + 1) : false;
+        ++n_vis;
+        return true;
+    };
+    // Lanes run through coalescence checks and jumps on their own until each needs
+    // to step through a tile (or is done); then every lane that needs to walks its
+    // tile at once, in lockstep: divergent lanes never serialise their walks.
+    TileMeta m;
+    bool run = true, walk = false;
     for (;;) {
-        const TileMeta m = ring[0];
+        while (run && !walk) {
+            m = ring[0];
 #pragma unroll
-        for (int k = 0; k + 1 < FIX_AHEAD; ++k) ring[k] = ring[k + 1];
-        ring[FIX_AHEAD - 1] = ld(tile_at(i + FIX_AHEAD));
-        if (__double_as_longlong(m.old) == __double_as_longlong(att)) break;  // coalesced
-        const int64_t g = st.g0 + i;
-        tst[g] = att;
-        double x;
-        SegDesc d;
-        d.mx = m.mx;
-        d.e0 = m.mx > 0.0 ? binade(m.mx) : 0;
+            for (int k = 0; k + 1 < FIX_AHEAD; ++k) ring[k] = ring[k + 1];
+            ring[FIX_AHEAD - 1] = ld(ci + FIX_AHEAD);
+            if (__double_as_longlong(m.old) == __double_as_longlong(att)) {  // coalesced
+                run = false;
+                break;
+            }
+            tst[ci] = att;
+            double x;
+            SegDesc d;
+            d.mx = m.mx;
+            d.e0 = binade(m.mx);
 #pragma unroll
-        for (int k = 0; k < 2 * JB; ++k) d.q[k] = m.q[k];
-        if (!(m.mx > 0.0)) {
-            ++n_held;  // inactive tile: held
-        } else if (a.jumps && release_jump(d, att, &x)) {
-            att = x;
-            jumped += T;
-        } else {
+            for (int k = 0; k < 2 * JB; ++k) d.q[k] = m.q[k];
+            if (a.jumps && release_jump(d, att, &x)) {
+                att = x;
+                jumped += T;
+                run = next();
+            } else {
+                walk = true;
+            }
+        }
+        if (!__any(walk)) break;
+        if (walk) {
             Walker<false> w;
             w.att = att;
             w.bs = bs;
-            w.ntiles = 1;
-            stream_col<false>(p, cur, (uint32_t)(i * T), T, T, w);
+            w.i0 = 0;
+            w.nst = 1;
+            const uint32_t off = tile_off(a, m.g);
+            stream_col<true, WNB>(p, [&](int) { return off; }, 1, T, w);  // (the walking lanes step the same rows)
             att = w.att;
             walked += T;
+            walk = false;
+            run = next();
         }
-        if (++i < st.ntiles) continue;
-        // the end of cur: publish, continue into the successor if it can be claimed
-        st_sc1(end + cur, att);
-        if (nx < 0 || !comp_claim(a, b, nx)) break;  // last active one / its owner read an older end (flagged)
-        if (!sn_ok) sn = super_of(a, nx);
-        cur = nx;
-        st = sn;
-        a.start[b][cur] = att;
-        nx = nxt[cur];
-        sn_ok = false;
-        i = 0;
-        ++n_vis;
     }
     if (a.trace && a.sweep_idx < 16) {
         uint32_t *r = a.trace + (((int64_t)a.sweep_idx * 3 + b) * a.GS + s) * 5;
         r[0] = (uint32_t)(wall_clock64() - t_start);  // 100 MHz ticks
         r[1] = (uint32_t)(walked / a.T);
         r[2] = (uint32_t)(jumped / a.T);
-        r[3] = (uint32_t)n_held;
+        r[3] = 0;
         r[4] = (uint32_t)n_vis;
     }
     if (walked) atomicAdd(a.walked, (unsigned long long)walked);
@@ -810,8 +824,7 @@ __global__ void __launch_bounds__(192, MM_APPLY_MINB) comp_apply_kernel(CompArgs
     const int len = valid ? (int)min((int64_t)T, a.N_proc - g * T) : 0;
     const BandStep bs = band_step(a, b);
     const short2 *X = a.band[b];
-    // this tile's column and rows in the M plane; its entry state: stored by the
-    // walks (active super-tile) or held since the previous active one's end
+    // this tile's column and rows in the M plane
     int64_t sg;
     int kg;
     tile_col(a, valid ? g : 0, &sg, &kg);
@@ -819,13 +832,10 @@ __global__ void __launch_bounds__(192, MM_APPLY_MINB) comp_apply_kernel(CompArgs
     const uint32_t e0 = col_elem(a, sg) + (uint32_t)(kg * T) * GS32;
     const double *Mp = a.Ms[b];
     double att = 0.0;
-    if (valid) {
-        if (a.act[b][sg]) {
-            att = a.tst[b][g];
-        } else {
-            const int32_t pv = a.prv[b][sg];
-            att = pv >= 0 ? a.end[b][pv] : 0.0;
-        }
+    if (valid) {  // the entry state of the tile, or of the next active one (held), or the chunk's end
+        const int64_t c = g / a.K;
+        const int32_t r = a.rank[b][g], na = a.nact[b][c];
+        att = r < na ? a.tstc[b][c * a.K + r] : na > 0 ? a.end[b][c * a.SPC + (na - 1) / a.TPS] : 0.0;
     }
     double gain = 1.0, gain_att = -1.0;  // gain of gain_att; att >= 0 never equals -1
     // a wave whose 64 tiles hold no active frame (the sparse band, almost

@@ -316,7 +316,7 @@ static int launch_eq(mm_ctx *c, int nsec, int ch, unsigned nblk, const EqArgs &e
 // successor may be stale) and exits at once if sweep k-1 flagged nothing.
 // Convergence is checked at the chain's single sync (evaluate_chain); a rare
 // unconverged batch is extended there (MM_COMP_SWEEPS sets the queued count).
-constexpr int COMP_SWEEPS = 6;  // queued per chain (a sweep after a quiet one exits at once; P_HOT on C2 needs 4-5)
+constexpr int COMP_SWEEPS = 8;  // queued per chain (a sweep after a quiet one exits at once; P_HOT on C2 needs 4-5)
 
 static int comp_sweeps(mm_ctx *c, int n) {
     CompArgs &ca = c->ca;
@@ -428,7 +428,7 @@ static int chain_check(mm_ctx *c, bool *converged) {
 // comp_super frames rounded to whole tiles), SPC super-tiles per chunk, nch chunks.
 static void comp_geometry(const mm_job *j, int64_t G, int *TPS, int64_t *SPC, int64_t *nch) {
     const int K = j->tiles_per_chunk;
-    *TPS = std::max(1, std::min((j->comp_super + j->tile / 2) / j->tile, 64));
+    *TPS = std::max(1, std::min((j->comp_super + j->tile / 2) / j->tile, P0_MAXL / 2));  // (a walk plus a warm-up super-tile)
     *nch = (G + K - 1) / K;
     *SPC = ((int64_t)K + *TPS - 1) / *TPS;
 }
@@ -483,15 +483,21 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     RET(get_buf(c, "q2", TG, &q2));
     ca.q_out = q2;
     *q2_out = q2;
-    double *st, *ends, *luts, *tst, *desc, *mmax;
+    double *st, *ends, *luts, *tstc, *descc, *mmax, *mmaxc;
     uint32_t *claims;
     RET(get_buf(c, "comp_start", (size_t)3 * NS, &st));
     RET(get_buf(c, "comp_end", (size_t)3 * NS, &ends));
     claims = c->ctl_claims;  // zeroed with the control block (sized by stage_front)
     RET(get_buf(c, "comp_lut", (size_t)3 * 32769, &luts));
-    RET(get_buf(c, "comp_tst", (size_t)3 * G, &tst));
+    const int64_t NC = nchunks * K;  // compact indices
     RET(get_buf(c, "comp_mmax", (size_t)3 * G, &mmax));
-    RET(get_buf(c, "comp_desc", (size_t)3 * DREC * G, &desc));
+    RET(get_buf(c, "comp_tstc", (size_t)3 * NC, &tstc));
+    RET(get_buf(c, "comp_mmaxc", (size_t)3 * NC, &mmaxc));
+    RET(get_buf(c, "comp_descc", (size_t)3 * DREC * NC, &descc));
+    int32_t *ranks, *tls, *nacts;
+    RET(get_buf(c, "comp_rank", (size_t)3 * G, &ranks));
+    RET(get_buf(c, "comp_tl", (size_t)3 * NC, &tls));
+    RET(get_buf(c, "comp_nact", (size_t)3 * nchunks, &nacts));
     ca.jumps = getenv("MM_COMP_NOJUMP") ? 0 : 1;  // diagnostics: results must not change
     unsigned int *changed = c->comp_changed;  // zeroed with the chain's control words
     ca.walked = reinterpret_cast<unsigned long long *>(c->ctl + RB_WALKED);
@@ -506,9 +512,8 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
         return set_err(c, MM_ERR_ARG, "track too long for one envelope solve (%lld frames): shard it by time",
                        (long long)j->frames_proc);
     ca.ms_bytes = (uint32_t)(ms_elems * 8);
-    int32_t *cnt, *tot, *links;
+    int32_t *cnt, *tot;
     RET(get_buf(c, "comp_cnt", (size_t)3 * G, &cnt));
-    RET(get_buf(c, "comp_links", (size_t)9 * NS, &links));
     tot = reinterpret_cast<int32_t *>(c->ctl + RB_TOTALS);  // zeroed and read back with the control block
     for (int b = 0; b < 3; ++b) {
         double *msb;
@@ -538,18 +543,23 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
         ca.cnt[b] = cnt + (size_t)b * G;
         ca.mmax[b] = mmax + (size_t)b * G;
         ca.total[b] = tot + (size_t)b * nchunks;
-        ca.tst[b] = tst + (size_t)b * G;
-        ca.act[b] = links + (size_t)b * NS;
-        ca.prv[b] = links + (size_t)(3 + b) * NS;
-        ca.nxt[b] = links + (size_t)(6 + b) * NS;
-        ca.desc[b] = desc + (size_t)b * DREC * G;
+        ca.rank[b] = ranks + (size_t)b * G;
+        ca.nact[b] = nacts + (size_t)b * nchunks;
+        ca.tl[b] = tls + (size_t)b * NC;
+        ca.mmaxc[b] = mmaxc + (size_t)b * NC;
+        ca.tstc[b] = tstc + (size_t)b * NC;
+        ca.descc[b] = descc + (size_t)b * DREC * NC;
         ca.start[b] = st + (size_t)b * NS;
         ca.end[b] = ends + (size_t)b * NS;
         ca.claim[b] = claims + (size_t)b * NS;
     }
     RET(launch(c, "comp_rms", comp_rms_kernel, dim3(nb, 3), dim3(256), 0, ca));
     RET(launch(c, "comp_links", comp_links_kernel, dim3((unsigned)nchunks, 3), dim3(1024), 0, ca));
-    RET(launch(c, "comp_pass0", comp_pass0_kernel, dim3(blocks_for(NS, PASS0_BLOCK), 3), dim3(2 * PASS0_BLOCK), 0, ca));
+    {
+        const unsigned wb = blocks_for(NS, PASS0_BLOCK);  // walker blocks, then describer blocks
+        RET(launch(c, "comp_pass0", comp_pass0_kernel, dim3(wb + blocks_for(G, PASS0_BLOCK), 3), dim3(PASS0_BLOCK), 0,
+                   ca, (int)wb));
+    }
     c->comp_on = true;
     c->ca = ca;
     c->comp_stamp = 0;
