@@ -107,10 +107,11 @@ def algorithmic_bytes(kernel, n, g, active, walked_per_launch):
         "eq": 8 * n + 4 * n,                  # f32 L,R in; int16 pair q1 out
         "pre_pointwise": 8 * n + 4 * n,
         "xover": 4 * n + 12 * n,              # q1 in; three int16-pair bands out
-        "comp_rms": 12 * n + 6 * n,           # bands in; uint16 rms x3 out
-        "comp_pass0": 6 * n,                  # uint16 rms of every band-frame (the table gathers hit L2)
-        "comp_fix": 2 * walked_per_launch,    # rms of the re-walked frames
-        "comp_apply": 6 * n + 12 * n + 4 * n,  # rms, bands in; mix out
+        "comp_rms": 12 * n + 24 * n,          # bands in; f64 M of every band-frame out (the M plane)
+        "comp_links": g * 3 * 8,              # active counts in; ranks out
+        "comp_pass0": 8 * active,             # M of every active band-frame
+        "comp_fix": 8 * walked_per_launch,    # M of the re-walked frames
+        "comp_apply": 8 * active + 12 * n + 4 * n,  # M of the active frames, bands in; mix out
         "kweight": 4 * n,                     # mix in
         "seg_reduce": g * 24,
         "gate": 0,
