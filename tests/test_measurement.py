@@ -12,19 +12,19 @@ sys.path.insert(0, ROOT)
 
 def test_c2_profile_matches_sources():
     import bench
-    with open(os.path.join(ROOT, "profiles", "r02_C2_pmc_summary.json")) as f:
+    with open(os.path.join(ROOT, "profiles", "r03_C2_pmc_summary.json")) as f:
         prof = json.load(f)
     assert prof["source_sha"] == bench.source_sha(), (
-        "profiles/r02_C2_pmc_summary.json was measured on other kernel sources: "
-        "re-run tools/pmc.sh r02 C2 on the GPU and tools/pmc_summary.py here")
+        "profiles/r03_C2_pmc_summary.json was measured on other kernel sources: "
+        "re-run tools/pmc.sh r03 C2 on the GPU and tools/pmc_summary.py here")
     # every chain kernel of the C2 bench has counters and a limiter
-    for k in ("eq", "xover", "comp_rms", "comp_compact", "comp_pass0", "comp_apply", "kweight", "finalize"):
+    for k in ("eq", "xover", "comp_rms", "comp_links", "comp_pass0", "comp_fix", "comp_apply", "kweight", "finalize"):
         assert prof["kernels"][k]["bytes_per_launch"] > 0 and prof["kernels"][k]["limiter"], k
 
 
 def test_bench_lines_carry_the_contract_fields():
-    for w in ("C2", "C2hot", "C3", "C4", "C5"):
-        with open(os.path.join(ROOT, "profiles", f"r02_bench_{w}.json")) as f:
+    for w in ("C1", "C2", "C2hot", "C3", "C4", "C5"):
+        with open(os.path.join(ROOT, "profiles", f"r03_bench_{w}.json")) as f:
             d = json.load(f)
         for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
                     "scaling", "vs_baseline", "dtype", "data", "config", "roofline"):
@@ -34,6 +34,6 @@ def test_bench_lines_carry_the_contract_fields():
         assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-12
         assert abs(d["value"] * d["ms_per_step"] / 1e3 - d["config"]["frames_per_rank_step"] * d["n_gpus"]) \
             <= 1e-6 * d["value"]
-    with open(os.path.join(ROOT, "profiles", "r02_bench_C2.json")) as f:
+    with open(os.path.join(ROOT, "profiles", "r03_bench_C2.json")) as f:
         c2 = json.load(f)
     assert c2["roofline"]["traffic"] is not None and c2["cpu_baseline"]["cores"] >= 1
