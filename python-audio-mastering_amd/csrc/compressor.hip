@@ -23,9 +23,9 @@
 //  3. comp_pass0 walker lanes (one per super-tile, a wave in lockstep) walk from a
 //                guess (the M of the first frame; exactly 0 at the chunk's first
 //                active tile), storing every tile's entry state and the end;
-//                describer lanes (one per active tile, on the idle SIMDs) record
-//                the exact effect of the tile's T release steps on any state of
-//                the four binades above its largest M (release jumps, below);
+//                comp_describe (one lane per active tile, launched before it)
+//                records the exact effect of the tile's T release steps on any
+//                state of the four binades above its largest M (release jumps);
 //  4. comp_fix   sweeps: a super-tile whose start differs from its predecessor's
 //                end re-walks from it tile by tile — jumped over pure-release
 //                tiles, stepped otherwise — and stops as soon as its state equals
@@ -556,38 +556,44 @@ __global__ void __launch_bounds__(1024) comp_links_kernel(CompArgs a) {
     if (tid == 1023) a.nact[b][c] = v;
 }
 
-// 3. speculative pass.  grid: (ceil(GS/64) + ceil(G/64), 3) of 64-lane blocks.
-//  * the first ceil(GS/64) blocks walk: lane = super-tile; the wave's 64 lanes
-//    step their tiles' rows in lockstep (their M-plane offsets staged in LDS).  A
-//    walker's start is exactly 0 for the chunk's first super-tile, else guessed:
-//    the M of its first frame (the state tracks M), or with `warmup` = 1 found by
-//    walking the previous super-tile from the M of its first frame.  Exactness
-//    never depends on the guess (the fix-up sweeps).
-//  * the other blocks describe: lane = tile; an active tile's release-jump record
-//    (beside the walkers on the otherwise idle SIMDs).
+// 3a. describers.  grid: (ceil(G/DESC_BLOCK), 3), lane = tile: an active tile's
+// release-jump record.  Its own launch (before pass 0), so its waves are not held to
+// the walkers' register budget: at ~100 VGPRs 4-5 describer waves share a SIMD,
+// where inside pass 0 they ran 2 per SIMD behind the walkers and set pass 0's time.
+#ifndef MM_DESC_NB
+#define MM_DESC_NB 1
+#endif
+constexpr int DESC_BLOCK = 256;
+
+__global__ void __launch_bounds__(DESC_BLOCK) comp_describe_kernel(CompArgs a) {
+    const int b = blockIdx.y;
+    const int64_t g = (int64_t)blockIdx.x * DESC_BLOCK + threadIdx.x;
+    const bool live = g < a.G && a.cnt[b][min(g, a.G - 1)] != 0;
+    if (__all(!live)) return;
+    const int64_t gc = min(g, a.G - 1);
+    Describer d;
+    d.bs = band_step(a, b);
+    const double mx = a.mmax[b][gc];
+    d.e0 = mx > 0.0 ? binade(mx) : 0;
+    const uint32_t off = tile_off(a, gc);
+    stream_col<true, MM_DESC_NB>(plane(a, b), [&](int) { return off; }, 1, a.T, d);
+    if (live) d.store(a.descc[b] + ((gc / a.K) * a.K + a.rank[b][gc]) * DREC);
+}
+
+// 3b. speculative pass.  grid: (ceil(GS/64), 3) of 64-lane blocks, lane =
+// super-tile; the wave's 64 lanes step their tiles' rows in lockstep (their
+// M-plane offsets staged in LDS).  A walker's start is exactly 0 for the chunk's
+// first super-tile, else guessed: the M of its first frame (the state tracks M),
+// or with `warmup` = 1 found by walking the previous super-tile from the M of its
+// first frame.  Exactness never depends on the guess (the fix-up sweeps).
 constexpr int PASS0_BLOCK = 64, P0_MAXL = 64;  // lanes; tiles per walker (warm-up included)
 
-__global__ void __launch_bounds__(PASS0_BLOCK) comp_pass0_kernel(CompArgs a, int walk_blocks) {
+__global__ void __launch_bounds__(PASS0_BLOCK) comp_pass0_kernel(CompArgs a) {
     __shared__ uint32_t offs_lds[P0_MAXL][PASS0_BLOCK];
     const int b = blockIdx.y;
     const BandStep bs = band_step(a, b);
     const Plane p = plane(a, b);
     const int lane = threadIdx.x;
-    if ((int)blockIdx.x >= walk_blocks) {  // describer
-        const int64_t g = ((int64_t)blockIdx.x - walk_blocks) * PASS0_BLOCK + lane;
-        const bool live = g < a.G && a.cnt[b][min(g, a.G - 1)] != 0 && a.jumps;
-        if (__all(!live)) return;
-        const int64_t gc = min(g, a.G - 1);
-        Describer d;
-        d.bs = bs;
-        const double mx = a.mmax[b][gc];
-        d.e0 = mx > 0.0 ? binade(mx) : 0;
-        const uint32_t off = tile_off(a, gc);
-        stream_col<true, P0_NB>(p, [&](int) { return off; }, 1, a.T, d);
-        if (live) d.store(a.descc[b] + ((gc / a.K) * a.K + a.rank[b][gc]) * DREC);
-        return;
-    }
-    __builtin_amdgcn_s_setprio(3);  // the walkers' chains first on SIMDs they share with describers
     const int64_t s = (int64_t)blockIdx.x * PASS0_BLOCK + lane;
     const int64_t sc = min(s, a.GS - 1);
     const Super st = super_of(a, b, sc);

@@ -555,11 +555,10 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     }
     RET(launch(c, "comp_rms", comp_rms_kernel, dim3(nb, 3), dim3(256), 0, ca));
     RET(launch(c, "comp_links", comp_links_kernel, dim3((unsigned)nchunks, 3), dim3(1024), 0, ca));
-    {
-        const unsigned wb = blocks_for(NS, PASS0_BLOCK);  // walker blocks, then describer blocks
-        RET(launch(c, "comp_pass0", comp_pass0_kernel, dim3(wb + blocks_for(G, PASS0_BLOCK), 3), dim3(PASS0_BLOCK), 0,
-                   ca, (int)wb));
-    }
+    if (ca.jumps)
+        RET(launch(c, "comp_describe", comp_describe_kernel, dim3(blocks_for(G, DESC_BLOCK), 3), dim3(DESC_BLOCK), 0,
+                   ca));
+    RET(launch(c, "comp_pass0", comp_pass0_kernel, dim3(blocks_for(NS, PASS0_BLOCK), 3), dim3(PASS0_BLOCK), 0, ca));
     c->comp_on = true;
     c->ca = ca;
     c->comp_stamp = 0;

@@ -31,15 +31,18 @@ EQ_PRESETS = {
 
 COMP_WARMUP = 0  # super-tiles of speculative warm-up walk before each one (none: the sweeps' jumps repair starts)
 COMP_MAX_ITERS = 100000
-# envelope solve unit in frames at 44.1 kHz.  The envelope's time constants are in
-# ms (attack/release frames scale with the rate), so the unit scales with it.
+# envelope solve unit in frames, at EVERY rate: 8 tiles of 125.  It is not scaled
+# with the rate: with 8 tiles per super-tile the 64 lanes (tiles) of a comp_rms wave
+# cover 8 whole super-tiles, so each M-plane store writes 8 runs of 64 B; at 96 kHz
+# the rate-scaled 17 tiles scattered them over ~64 lines (C5 21.2 -> 18.2 ms per
+# step).
 COMP_SUPER_FRAMES = 1000
 
 
 def comp_super_frames(rate: int, tile: int = design.DEFAULT_TILE) -> int:
-    """Super-tile length for `rate` in frames: whole tiles (the device rounds to
-    tiles; 8 x 125 at 44.1 kHz)."""
-    return max(1, int(round(COMP_SUPER_FRAMES * rate / 44100 / tile))) * tile
+    """Super-tile length in frames: whole tiles (8 x 125 at every rate)."""
+    del rate  # (see COMP_SUPER_FRAMES)
+    return max(1, int(round(COMP_SUPER_FRAMES / tile))) * tile
 
 
 class Job:

@@ -18,7 +18,8 @@ def test_c2_profile_matches_sources():
         "profiles/r03_C2_pmc_summary.json was measured on other kernel sources: "
         "re-run tools/pmc.sh r03 C2 on the GPU and tools/pmc_summary.py here")
     # every chain kernel of the C2 bench has counters and a limiter
-    for k in ("eq", "xover", "comp_rms", "comp_links", "comp_pass0", "comp_fix", "comp_apply", "kweight", "finalize"):
+    for k in ("eq", "xover", "comp_rms", "comp_links", "comp_describe", "comp_pass0", "comp_fix", "comp_apply", "kweight",
+              "finalize"):
         assert prof["kernels"][k]["bytes_per_launch"] > 0 and prof["kernels"][k]["limiter"], k
 
 
