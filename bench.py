@@ -89,7 +89,8 @@ def source_sha() -> str:
     """Hash of everything that shapes the kernels' work (HIP sources, header, host
     geometry): a profile under profiles/ is used only for the exact same code."""
     h = hashlib.sha256()
-    files = sorted(glob.glob(os.path.join(ROOT, "python-audio-mastering_amd", "csrc", "*")))
+    csrc = os.path.join(ROOT, "python-audio-mastering_amd", "csrc")
+    files = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.h")))
     files += [os.path.join(ROOT, "include", "mastering.h"),
               os.path.join(ROOT, "python-audio-mastering_amd", "mastering_amd", "engine.py"),
               os.path.join(ROOT, "python-audio-mastering_amd", "mastering_amd", "design.py")]

@@ -131,12 +131,35 @@ typedef struct mm_result {
     int64_t comp_jumped;     /* frames the sweeps crossed by exact release jumps */
 } mm_result;
 
+/* Geometry of the compressor's envelope solve for a job (mm_solve_geometry: the
+   planning arithmetic stage C runs on, computed on the host without a GPU). */
+typedef struct mm_solve_geom {
+    int32_t tps;             /* tiles per super-tile (a walker's unit)          */
+    int32_t tile_rows;       /* M-plane rows per tile: T rounded up to whole walk
+                                load blocks (extra rows hold M = 0)            */
+    int32_t rows;            /* rows per column: tps * tile_rows + prefetch pad  */
+    int32_t _pad;
+    int64_t cols_per_chunk;  /* super-tile columns per chunk (whole blocks of 64) */
+    int64_t chunks;
+    int64_t chunk_plane_bytes; /* one chunk's part of one band's M plane: walked
+                                through 32-bit buffer offsets, < 2^31           */
+    int64_t plane_bytes;     /* the three bands' M planes of the whole track     */
+} mm_solve_geom;
+
 /* ---- context ------------------------------------------------------------ */
 int mm_create(int device, mm_ctx **ctx);
 int mm_destroy(mm_ctx *ctx);
 const char *mm_last_error(mm_ctx *ctx);
 int mm_sync(mm_ctx *ctx);
+/* ABI version: 2 = mm_band.lut_key and mm_result.comp_jumped (round 3),
+   mm_solve_geometry (round 4).  A caller built against an older header must
+   refuse a library whose version differs from its own MM_ABI_VERSION. */
+#define MM_ABI_VERSION 2
 int mm_version(void);
+/* The envelope-solve geometry of a job (no context, no GPU).  MM_ERR_ARG if a
+   chunk's plane would not fit 32-bit offsets (no track length below 2^31 frames
+   at rates up to 192 kHz does). */
+int mm_solve_geometry(const mm_job *job, mm_solve_geom *out);
 /* sha256 prefix (16 hex digits) of the sources this library was built from
    (mastering_amd/srcsha.py: the csrc sources and this header) */
 const char *mm_source_sha(void);

@@ -135,7 +135,7 @@ struct CompArgs {
     int64_t N_proc, G;
     int T, K, ch, warmup;
     int TPS;                   // tiles per super-tile (envelope solve unit)
-    int64_t SPC;               // super-tiles per chunk = ceil(K / TPS)
+    int64_t SPC;               // super-tiles (columns) per chunk: ceil(K / TPS) rounded up to a multiple of 64
     int64_t GS;                // super-tiles = chunks * SPC
     const short2 *band[3];
     const double *lut[3];      // device tables [32769]: M per integer rms
@@ -144,17 +144,20 @@ struct CompArgs {
     double attack_frames[3], release_frames[3];
     double rcp_attack[3], rcp_release[3];
     double *Ms[3];             // super-tile-major M plane, column blocks of 64 x RP rows (compressor.hip tile_col)
-    int RP;                    // rows per column of the M plane (TPS*T + prefetch padding)
-    uint32_t ms_bytes;         // bytes of one band's M plane (buffer descriptors: < 4 GB)
+    int TP;                    // plane rows per tile: T rounded up to whole walk load blocks
+    int RP;                    // rows per column of the M plane (TPS*TP + prefetch padding)
+    int64_t chunk_elems;       // elements of one chunk's part of a band's plane (buffer descriptors: < 4 GB)
     const double *E[3], *tail[3];  // per tile: sum of L^2+R^2, and over its last look % T frames
     int32_t *cnt[3];           // per tile: active frames
     double *mmax[3];           // per tile: largest M
+    double *ced[3];            // per tile: (max,+) release summary {c, D} (double2; comp_rms)
     int32_t *total[3];         // per chunk: active frames (statistics)
     int32_t *rank[3];          // per tile: active tiles before it in its chunk (comp_links)
     int32_t *nact[3];          // per chunk: active tiles
     // per active tile at compact index ci = chunk * K + rank:
     int32_t *tl[3];            // the tile
     double *mmaxc[3];          // its largest M
+    double *cedc[3];           // its (max,+) release summary (double2; pass-0 guesses)
     double *tstc[3];           // envelope state on entry (written by the owning walks)
     double *descc[3];          // release-jump record [2 JB] (compressor.hip Describer)
     double *start[3];          // per-super-tile start state
@@ -165,7 +168,7 @@ struct CompArgs {
     int heads;                 // 0: Jacobi sweep (every stale super-tile walks); 1: run heads only
     unsigned int *changed;
     unsigned long long *walked;  // [0] frames re-walked, [1] frames jumped by the fix-up sweeps (statistics)
-    uint32_t *trace;           // diagnostics (MM_FIX_TRACE): per sweep, band, super-tile {10 ns ticks, walked, jumped, held, visited}
+    uint32_t *trace;           // diagnostics (MM_FIX_TRACE): per sweep, band, super-tile {10 ns ticks, walked, jumped, visited}
     int sweep_idx;
     short2 *q_out;
 };

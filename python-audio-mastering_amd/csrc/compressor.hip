@@ -21,8 +21,9 @@
 //                count and largest M;
 //  2. comp_links per (chunk, band): ranks and lists the active tiles;
 //  3. comp_pass0 walker lanes (one per super-tile, a wave in lockstep) walk from a
-//                guess (the M of the first frame; exactly 0 at the chunk's first
-//                active tile), storing every tile's entry state and the end;
+//                guess (the (max,+) release envelope of the preceding active
+//                tiles; exactly 0 at the chunk's first active tile), storing every
+//                tile's entry state and the end;
 //                comp_describe (one lane per active tile, launched before it)
 //                records the exact effect of the tile's T release steps on any
 //                state of the four binades above its largest M (release jumps);
@@ -66,34 +67,55 @@ __device__ __forceinline__ uint32_t rms_exact(double S, double n, float inv_n) {
 constexpr int RMS_B = 8;  // frames per load block of comp_rms
 
 // Super-tile-major M plane of a band: frame n of tile g — the k-th tile of
-// super-tile s — is row k*T + n of column s.  Columns come in blocks of 64 (one
-// pass-0 wave): element (s, row) at ((s / 64) * RP + row) * 64 + s % 64, RP =
-// TPS*T + WALK_PAD rows (prefetch padding), so the 64 walkers of a wave read 512
-// contiguous bytes at every step and a column's rows lie 512 B apart (a tile's
-// rows and a block's walks stay within a few pages).
+// super-tile s — is row k*TP + n of column s (TP = T rounded up to whole walk load
+// blocks; rows past a tile's frames hold M = 0, identity steps).  Columns come in
+// blocks of 64 (one pass-0 wave): element (s, row) at ((s / 64) * RP + row) * 64 +
+// s % 64, RP = TPS*TP + WALK_PAD rows (prefetch padding), so the 64 walkers of a
+// wave read 512 contiguous bytes at every step and a column's rows lie 512 B apart
+// (a tile's rows and a block's walks stay within a few pages).  Each chunk's
+// columns (SPC, whole column blocks) form a plane of their own, chunk_elems
+// elements from the chunk's base: offsets within it fit 32 bits at any track
+// length (every kernel that walks it does so within one chunk per wave).
 __device__ __forceinline__ void tile_col(const CompArgs &a, int64_t g, int64_t *s, int *k) {
     const int64_t c = g / a.K, j = g - c * a.K;
     *s = c * a.SPC + j / a.TPS;
     *k = (int)(j - (j / a.TPS) * a.TPS);
 }
-// element index of row 0 of column s
+// element index of row 0 of column s within its chunk's plane
 __device__ __forceinline__ uint32_t col_elem(const CompArgs &a, int64_t s) {
-    return (uint32_t)((s >> 6) * (int64_t)a.RP * 64 + (s & 63));
+    const int64_t sl = s % a.SPC;
+    return (uint32_t)((sl >> 6) * (int64_t)a.RP * 64 + (sl & 63));
+}
+// chunk c's plane of band b
+__device__ __forceinline__ double *chunk_plane(const CompArgs &a, int b, int64_t c) {
+    return a.Ms[b] + c * a.chunk_elems;
 }
 
-// 1. rms and M per frame.  grid: (ceil(G/256), 3 bands), lane = tile.  The
-// window [max(chunk0, f-look), f) slides one frame per step: + frame f-1 (this
-// lane's own previous frame), - frame f-1-look (up to ~4 tiles back: another
-// lane's data, coalesced across the wave).  The window sum is an exact integer
-// held in a double.  M = lut[r] is gathered ONCE here (a block of RMS_B frames'
-// gathers is stored one block later) and written to the super-tile-major plane
-// that the walkers and comp_apply read; rows past the end of a partial last tile
-// get M = 0 (identity steps).  Also the tile's active count and largest M (the
-// table is nondecreasing in r) and the per-chunk active count.
+// 1. rms and M per frame.  grid: (GS * TPS / 256, 3 bands) of 256-thread blocks,
+// one wave per (column block, position k): wave v handles tile k = v % TPS of the 64
+// super-tiles (columns) of column block v / TPS, lane l the one of column 64 (v /
+// TPS) + l.  SPC is a multiple of 64, so a column block lies in one chunk and the
+// wave's 64 lanes store row k*T + n of 64 consecutive columns: every M store is
+// one 512-byte run (round 3 mapped lanes to consecutive tiles: 8 runs of 64 B per
+// store).  The band loads are TPS tiles apart across the lanes (the block's TPS
+// waves share those lines).  The window [max(chunk0, f-look), f) slides one frame
+// per step: + frame f-1 (this lane's own previous frame), - frame f-1-look (up to
+// ~4 tiles back: another tile's data).  The window sum is an exact integer held in
+// a double.  M = lut[r] is gathered ONCE here (a block of RMS_B frames' gathers is
+// stored one block later) and written to the super-tile-major plane that the
+// walkers and comp_apply read; rows past the end of a partial last tile get M = 0
+// (identity steps).  Also the tile's active count and largest M (the table is
+// nondecreasing in r), its (max,+) release summary for the pass-0 guesses, and the
+// per-chunk active count.
 __global__ void __launch_bounds__(256) comp_rms_kernel(CompArgs a) {
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int b = blockIdx.y;
-    if (g >= a.G) return;
+    const int64_t wv = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int kc = (int)(wv % a.TPS);
+    const int64_t sc = (wv / a.TPS) * 64 + (threadIdx.x & 63);
+    const int64_t cc = sc / a.SPC;
+    const int64_t jt = (sc - cc * a.SPC) * a.TPS + kc;
+    const int64_t g = cc * a.K + jt;
+    if (jt >= a.K || g >= a.G) return;  // past the chunk's tiles (its last super-tile) or the track
     const short2 *x = a.band[b];
     const int look = a.look[b];
     const int T = a.T;
@@ -122,12 +144,10 @@ __global__ void __launch_bounds__(256) comp_rms_kernel(CompArgs a) {
     float inv = n > 0.0 ? 1.0f / (float)n : 0.f;
     const uint32_t r0 = a.r0[b];
     const double *lut = a.lut[b];
-    int64_t sc;
-    int kc;
-    tile_col(a, g, &sc, &kc);
+    const double rR = a.rcp_release[b];
     constexpr uint32_t GS32 = 64;  // elements per row of a column block
-    double *Mo = a.Ms[b];
-    uint32_t e = col_elem(a, sc) + (uint32_t)(kc * T) * GS32;  // row k*T of column s
+    double *Mo = chunk_plane(a, b, cc);
+    uint32_t e = col_elem(a, sc) + (uint32_t)(kc * a.TP) * GS32;  // row k*TP of column s
     int i_proc = 0, active = 0;
     uint32_t rmx = 0;
     struct Pair {
@@ -162,11 +182,22 @@ __global__ void __launch_bounds__(256) comp_rms_kernel(CompArgs a) {
     Pair buf[NB][B];
     double mq[B];
     int pn = 0;  // rows of the pending block (its gathers in flight)
+    // (max,+) release summary of the tile: any state E on entry leaves it at most at
+    // max(ce, E - De) when every attack is taken as an instant clamp (dec ~ M/R; a
+    // guess only, so not correctly rounded)
+    double ce = 0.0, De = 0.0;
     // store the pending block: whole (every block but a partial last one) or its pn rows
     auto flush = [&](bool whole) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < B; ++j)
-            if (whole || j < pn) Mo[e + (uint32_t)j * GS32] = mq[j];
+            if (whole || j < pn) {
+#ifndef MM_RMS_NOSTORE  // (timing experiment only: no M plane)
+                Mo[e + (uint32_t)j * GS32] = mq[j];
+#endif
+                const double d = mq[j] * rR;
+                ce = fmax(mq[j], ce - d);
+                De += d;
+            }
         e += (uint32_t)pn * GS32;
     };
     if (len > 0) {
@@ -215,14 +246,17 @@ __global__ void __launch_bounds__(256) comp_rms_kernel(CompArgs a) {
         }
         flush(false);
     }
-    // rows past a partial last tile's frames: M = 0 (identity steps)
-    for (int i = max(len, 0); i < T; ++i, e += GS32) Mo[e] = 0.0;
+    // rows past the tile's frames (a partial last tile, the padding to TP): M = 0
+    // (identity steps)
+    for (int i = max(len, 0); i < a.TP; ++i, e += GS32) Mo[e] = 0.0;
     a.cnt[b][g] = active;
     a.mmax[b][g] = lut[rmx];
+    reinterpret_cast<double2 *>(a.ced[b])[g] = make_double2(ce, De);
     // per-chunk active count (statistics): one atomic per wave when all 64 lanes
-    // are live (lanes past G exited above) and their tiles share a chunk
-    const int c = (int)(g / a.K);
-    if (__ballot(1) == ~0ull && __all(c == __builtin_amdgcn_readfirstlane(c))) {
+    // are live (lanes past the chunk's tiles or G exited above; the wave's tiles
+    // share a chunk)
+    const int c = (int)cc;
+    if (__ballot(1) == ~0ull) {
         int v = active;
         for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
         if (__lane_id() == 0 && v) atomicAdd(a.total[b] + c, v);
@@ -321,7 +355,7 @@ __device__ __forceinline__ Super super_of(const CompArgs &a, int b, int64_t s) {
 #ifndef MM_WALK_NB
 #define MM_WALK_NB 2
 #endif
-constexpr int WB = MM_WALK_B;   // rows per load block (divides T: checked on the host)
+constexpr int WB = MM_WALK_B;   // rows per load block (divides TP)
 constexpr int WNB = MM_WALK_NB; // blocks in flight (sweep walkers)
 #ifndef MM_P0_NB
 #define MM_P0_NB 2
@@ -337,18 +371,21 @@ struct Plane {
     int RP;
 };
 constexpr uint32_t ROWB = 64u * 8u;  // bytes per row of a column block
-__device__ __forceinline__ Plane plane(const CompArgs &a, int b) {
+// (c: the wave's chunk, made uniform here: the descriptor lives in SGPRs)
+__device__ __forceinline__ Plane plane(const CompArgs &a, int b, int64_t c) {
     Plane p;
-    p.r = __builtin_amdgcn_make_buffer_rsrc(a.Ms[b], (short)0, (int)a.ms_bytes, 0x00020000);
+    const int64_t cu = ((int64_t)__builtin_amdgcn_readfirstlane((int)(c >> 32)) << 32) |
+                       (uint32_t)__builtin_amdgcn_readfirstlane((int)(c & 0xffffffff));
+    p.r = __builtin_amdgcn_make_buffer_rsrc(chunk_plane(a, b, cu), (short)0, (int)(a.chunk_elems * 8), 0x00020000);
     p.RP = a.RP;
     return p;
 }
-// byte offset of row 0 of tile g (its column and row k*T)
+// byte offset of row 0 of tile g (its column and row k*TP) in its chunk's plane
 __device__ __forceinline__ uint32_t tile_off(const CompArgs &a, int64_t g) {
     int64_t s;
     int k;
     tile_col(a, g, &s, &k);
-    return (col_elem(a, s) + (uint32_t)(k * a.T) * 64u) * 8u;
+    return (col_elem(a, s) + (uint32_t)(k * a.TP) * 64u) * 8u;
 }
 __device__ __forceinline__ double ld_plane(const Plane &p, uint32_t vo, uint32_t so) {
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(p.r, vo, so, 0));
@@ -550,6 +587,7 @@ __global__ void __launch_bounds__(1024) comp_links_kernel(CompArgs a) {
         if (a.cnt[b][g] != 0) {
             a.tl[b][g0 + r] = (int32_t)g;
             a.mmaxc[b][g0 + r] = a.mmax[b][g];
+            reinterpret_cast<double2 *>(a.cedc[b])[g0 + r] = reinterpret_cast<const double2 *>(a.ced[b])[g];
             ++r;
         }
     }
@@ -565,34 +603,42 @@ __global__ void __launch_bounds__(1024) comp_links_kernel(CompArgs a) {
 #endif
 constexpr int DESC_BLOCK = 256;
 
+// Lanes map to tiles as in comp_rms (a wave: one tile position of 64 columns of one
+// chunk), so every step's loads are one 512-byte run.
 __global__ void __launch_bounds__(DESC_BLOCK) comp_describe_kernel(CompArgs a) {
     const int b = blockIdx.y;
-    const int64_t g = (int64_t)blockIdx.x * DESC_BLOCK + threadIdx.x;
-    const bool live = g < a.G && a.cnt[b][min(g, a.G - 1)] != 0;
+    const int64_t wv = (int64_t)blockIdx.x * (DESC_BLOCK / 64) + (threadIdx.x >> 6);
+    const int kc = (int)(wv % a.TPS);
+    const int64_t sc = (wv / a.TPS) * 64 + (threadIdx.x & 63);
+    const int64_t cc = sc / a.SPC;
+    const int64_t jt = (sc - cc * a.SPC) * a.TPS + kc;
+    const int64_t g = cc * a.K + jt;
+    const bool live = jt < a.K && g < a.G && a.cnt[b][min(g, a.G - 1)] != 0;
     if (__all(!live)) return;
-    const int64_t gc = min(g, a.G - 1);
+    const int64_t gc = live ? g : cc * a.K;  // (dead lanes: the chunk's first tile)
     Describer d;
     d.bs = band_step(a, b);
     const double mx = a.mmax[b][gc];
     d.e0 = mx > 0.0 ? binade(mx) : 0;
     const uint32_t off = tile_off(a, gc);
-    stream_col<true, MM_DESC_NB>(plane(a, b), [&](int) { return off; }, 1, a.T, d);
-    if (live) d.store(a.descc[b] + ((gc / a.K) * a.K + a.rank[b][gc]) * DREC);
+    stream_col<true, MM_DESC_NB>(plane(a, b, cc), [&](int) { return off; }, 1, a.TP, d);
+    if (live) d.store(a.descc[b] + (cc * a.K + a.rank[b][gc]) * DREC);
 }
 
 // 3b. speculative pass.  grid: (ceil(GS/64), 3) of 64-lane blocks, lane =
 // super-tile; the wave's 64 lanes step their tiles' rows in lockstep (their
 // M-plane offsets staged in LDS).  A walker's start is exactly 0 for the chunk's
-// first super-tile, else guessed: the M of its first frame (the state tracks M),
-// or with `warmup` = 1 found by walking the previous super-tile from the M of its
-// first frame.  Exactness never depends on the guess (the fix-up sweeps).
+// first super-tile, else guessed: the (max,+) release envelope of the E_TILES
+// active tiles before it (with `warmup` = 1, before a walk of the previous
+// super-tile).  Exactness never depends on the guess (the fix-up sweeps).
 constexpr int PASS0_BLOCK = 64, P0_MAXL = 64;  // lanes; tiles per walker (warm-up included)
+constexpr int E_TILES = 64;  // active tiles folded into a pass-0 guess (~8000 frames of release history)
 
 __global__ void __launch_bounds__(PASS0_BLOCK) comp_pass0_kernel(CompArgs a) {
     __shared__ uint32_t offs_lds[P0_MAXL][PASS0_BLOCK];
     const int b = blockIdx.y;
     const BandStep bs = band_step(a, b);
-    const Plane p = plane(a, b);
+    const Plane p = plane(a, b, (int64_t)blockIdx.x * PASS0_BLOCK / a.SPC);  // (a block's 64 columns: one chunk)
     const int lane = threadIdx.x;
     const int64_t s = (int64_t)blockIdx.x * PASS0_BLOCK + lane;
     const int64_t sc = min(s, a.GS - 1);
@@ -610,8 +656,26 @@ __global__ void __launch_bounds__(PASS0_BLOCK) comp_pass0_kernel(CompArgs a) {
     for (int i = 0; i < nmax; ++i)  // the walk's tile offsets (lanes past their own repeat their last)
         offs_lds[i][lane] = tile_off(a, ntot ? tl[cw0 + min(i, ntot - 1)] : 0);
     __syncthreads();
+    // the guess: the (max,+) envelope bound over the E_TILES active tiles before the
+    // walk (every attack an instant clamp, release at ~M/R per frame: the state
+    // after a loud stretch decays from its peak, where the M of the first frame
+    // left ~all super-tiles stale)
     double att = 0.0;
-    if (live && cw0 != cK) att = ld_plane(p, offs_lds[0][lane], 0);  // the M of the walk's first frame
+    if (live && cw0 != cK) {
+        const double2 *cd = reinterpret_cast<const double2 *>(a.cedc[b]);
+        int64_t i = max(cK, cw0 - E_TILES);
+        for (; i + 8 <= cw0; i += 8) {
+            double2 v[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[q] = cd[i + q];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) att = fmax(v[q].x, att - v[q].y);
+        }
+        for (; i < cw0; ++i) {
+            const double2 v = cd[i];
+            att = fmax(v.x, att - v.y);
+        }
+    }
     Walker<true> w;
     w.att = att;
     w.out = att;
@@ -620,7 +684,7 @@ __global__ void __launch_bounds__(PASS0_BLOCK) comp_pass0_kernel(CompArgs a) {
     w.tst = a.tstc[b] + st.ci0;
     w.i0 = nwarm;
     w.nst = live ? st.ntiles : 0;
-    stream_col<true, P0_NB>(p, [&](int i) { return offs_lds[i][lane]; }, nmax, a.T, w);
+    stream_col<true, P0_NB>(p, [&](int i) { return offs_lds[i][lane]; }, nmax, a.TP, w);
     if (live) {
         a.start[b][s] = w.sv;
         a.end[b][s] = w.out;
@@ -690,7 +754,7 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
     const uint64_t t_start = a.trace ? wall_clock64() : 0;
     int n_vis = 1;
     const BandStep bs = band_step(a, b);
-    const Plane p = plane(a, b);
+    const Plane p = plane(a, b, s / a.SPC);  // (the wave's 64 columns and their walks: one chunk)
     double *tst = a.tstc[b];
     const int T = a.T;
     int64_t walked = 0, jumped = 0;
@@ -771,7 +835,7 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
             w.i0 = 0;
             w.nst = 1;
             const uint32_t off = tile_off(a, m.g);
-            stream_col<true, WNB>(p, [&](int) { return off; }, 1, T, w);  // (the walking lanes step the same rows)
+            stream_col<true, WNB>(p, [&](int) { return off; }, 1, a.TP, w);  // (the walking lanes step the same rows)
             att = w.att;
             walked += T;
             walk = false;
@@ -779,12 +843,11 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
         }
     }
     if (a.trace && a.sweep_idx < 16) {
-        uint32_t *r = a.trace + (((int64_t)a.sweep_idx * 3 + b) * a.GS + s) * 5;
+        uint32_t *r = a.trace + (((int64_t)a.sweep_idx * 3 + b) * a.GS + s) * 4;
         r[0] = (uint32_t)(wall_clock64() - t_start);  // 100 MHz ticks
         r[1] = (uint32_t)(walked / a.T);
         r[2] = (uint32_t)(jumped / a.T);
-        r[3] = 0;
-        r[4] = (uint32_t)n_vis;
+        r[3] = (uint32_t)n_vis;
     }
     if (walked) atomicAdd(a.walked, (unsigned long long)walked);
     if (jumped) atomicAdd(a.walked + 1, (unsigned long long)jumped);
@@ -835,8 +898,8 @@ __global__ void __launch_bounds__(192, MM_APPLY_MINB) comp_apply_kernel(CompArgs
     int kg;
     tile_col(a, valid ? g : 0, &sg, &kg);
     constexpr uint32_t GS32 = 64;  // elements per row of a column block
-    const uint32_t e0 = col_elem(a, sg) + (uint32_t)(kg * T) * GS32;
-    const double *Mp = a.Ms[b];
+    const uint32_t e0 = col_elem(a, sg) + (uint32_t)(kg * a.TP) * GS32;
+    const double *Mp = chunk_plane(a, b, valid ? g / a.K : 0);
     double att = 0.0;
     if (valid) {  // the entry state of the tile, or of the next active one (held), or the chunk's end
         const int64_t c = g / a.K;
@@ -900,7 +963,12 @@ __global__ void __launch_bounds__(192, MM_APPLY_MINB) comp_apply_kernel(CompArgs
                 for (int j = 0; j < S; ++j) gj[j] = gain;
             } else {
 #pragma unroll
-                for (int j = 0; j < S; ++j) gj[j] = exp10(neg_div20(at[j]));  // db_to_float(-att); exp10(-0) == 1 exactly
+                for (int j = 0; j < S; ++j)
+#ifdef MM_APPLY_NOEXP  // timing experiment only (wrong gains)
+                    gj[j] = 1.0 + neg_div20(at[j]);
+#else
+                    gj[j] = exp10(neg_div20(at[j]));  // db_to_float(-att); exp10(-0) == 1 exactly
+#endif
                 gain = gj[S - 1];
                 gain_att = at[S - 1];
             }

@@ -63,8 +63,7 @@ struct mm_ctx {
     char *ctl = nullptr;                // the chain's control block (setup_control)
     uint32_t *ctl_claims = nullptr;     // its zeroed claim stamps
     int comp_iters = 0, comp_pending = 0;
-    uint32_t chain_tag = 0;  // per-chain tag of the release-jump marks (compressor.hip)
-    unsigned comp_nb = 0;
+    int comp_queue = 0;  // sweeps to queue with the next solve (0: COMP_SWEEPS; then the last solve's need + 1)
     // loudness on the device
     double *gate_out = nullptr;         // [2]: L, gain
     std::vector<int64_t> geom_cache;    // loudness geometry already on the device
@@ -128,15 +127,6 @@ static int get_buf(mm_ctx *c, const char *name, size_t count, T **out) {
         b.cap = bytes;
     }
     *out = reinterpret_cast<T *>(b.p);
-    return MM_OK;
-}
-
-// get_buf whose storage is zeroed (on the stream) whenever it is (re)allocated
-template <typename T>
-static int get_buf_zeroed(mm_ctx *c, const char *name, size_t count, T **out) {
-    const size_t before = c->bufs[name].cap;
-    RET_EARLY(get_buf(c, name, count, out));
-    if (c->bufs[name].cap != before) HIPCHK(c, hipMemsetAsync(*out, 0, c->bufs[name].cap, c->stream));
     return MM_OK;
 }
 
@@ -264,7 +254,6 @@ static int validate(mm_ctx *c, const mm_job *j) {
         return set_err(c, MM_ERR_ARG, "K-weighting tables built for %d-frame tiles", j->kweight.tile);
     if (j->multiband_on) {
         if (j->xover.nsec != 4 || j->xover.nsec_branch0 != 2) return set_err(c, MM_ERR_ARG, "crossover must be 2+2 sections");
-        if (j->tile % WB != 0) return set_err(c, MM_ERR_ARG, "the envelope solve needs tiles of a multiple of %d frames", WB);
         for (int b = 0; b < 3; ++b) {
             if (!j->band[b].lut) return set_err(c, MM_ERR_ARG, "band %d: missing table", b);
             if (j->band[b].look < 0) return set_err(c, MM_ERR_ARG, "band %d: look < 0", b);
@@ -316,7 +305,7 @@ static int launch_eq(mm_ctx *c, int nsec, int ch, unsigned nblk, const EqArgs &e
 // successor may be stale) and exits at once if sweep k-1 flagged nothing.
 // Convergence is checked at the chain's single sync (evaluate_chain); a rare
 // unconverged batch is extended there (MM_COMP_SWEEPS sets the queued count).
-constexpr int COMP_SWEEPS = 8;  // queued per chain (a sweep after a quiet one exits at once; P_HOT on C2 needs 4-5)
+constexpr int COMP_SWEEPS = 8;  // queued by a context's first solve (a sweep after a quiet one exits at once)
 
 static int comp_sweeps(mm_ctx *c, int n) {
     CompArgs &ca = c->ca;
@@ -374,20 +363,21 @@ static int queue_readback(mm_ctx *c, bool lufs) {
 // block only waits on blocks that started before it) and whether the queued
 // sweeps converged.
 static int evaluate_chain(mm_ctx *c, bool *converged) {
-    if (getenv("MM_DEBUG_WALKED"))
+    static const bool debug_walked = getenv("MM_DEBUG_WALKED") != nullptr;
+    if (debug_walked)
         fprintf(stderr, "walked=%llu jumped=%llu\n", *reinterpret_cast<const unsigned long long *>(c->rb + RB_WALKED),
                 *reinterpret_cast<const unsigned long long *>(c->rb + RB_WALKED + 8));
     if (*reinterpret_cast<const unsigned *>(c->rb + RB_ERR)) return set_err(c, MM_ERR_STATE, "IIR look-back timed out");
     if (c->comp_on && c->ca.trace) {  // MM_FIX_TRACE: the three slowest walkers of every sweep
         const int64_t NS = c->ca.GS;
-        std::vector<uint32_t> tr((size_t)16 * 3 * NS * 5);
+        std::vector<uint32_t> tr((size_t)16 * 3 * NS * 4);
         HIPCHK(c, hipMemcpy(tr.data(), c->ca.trace, tr.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
         for (int k = 0; k < 16; ++k) {
             std::vector<std::pair<uint32_t, int64_t>> v;
             int64_t nw = 0;
             for (int64_t i = 0; i < 3 * NS; ++i) {
-                const uint32_t *r = &tr[((size_t)k * 3 * NS + i) * 5];
-                if (r[0] || r[4]) {
+                const uint32_t *r = &tr[((size_t)k * 3 * NS + i) * 4];
+                if (r[0] || r[3]) {
                     v.push_back({r[0], i});
                     ++nw;
                 }
@@ -396,10 +386,10 @@ static int evaluate_chain(mm_ctx *c, bool *converged) {
             std::sort(v.rbegin(), v.rend());
             fprintf(stderr, "sweep %d: %lld walkers;", k, (long long)nw);
             for (size_t q = 0; q < std::min<size_t>(3, v.size()); ++q) {
-                const uint32_t *r = &tr[((size_t)k * 3 * NS + v[q].second) * 5];
-                fprintf(stderr, " [band %lld st %lld: %.1f us walked %u jumped %u held %u visited %u]",
+                const uint32_t *r = &tr[((size_t)k * 3 * NS + v[q].second) * 4];
+                fprintf(stderr, " [band %lld st %lld: %.1f us walked %u jumped %u visited %u]",
                         (long long)(v[q].second / NS), (long long)(v[q].second % NS), r[0] / 100.0, r[1], r[2],
-                        r[3], r[4]);
+                        r[3]);
             }
             fprintf(stderr, "\n");
         }
@@ -412,6 +402,8 @@ static int evaluate_chain(mm_ctx *c, bool *converged) {
         c->comp_iters += k;
         *converged = k < c->comp_pending;
         c->comp_pending = 0;
+        // the solve needed comp_iters flagged sweeps and one quiet one: queue that + 1
+        if (*converged) c->comp_queue = std::min(16, std::max(3, c->comp_iters + 2));
         if (!*converged && c->comp_iters >= c->job.comp_max_iters)
             return set_err(c, MM_ERR_STATE, "compressor did not converge in %d sweeps", c->comp_iters);
     }
@@ -424,13 +416,24 @@ static int chain_check(mm_ctx *c, bool *converged) {
     return evaluate_chain(c, converged);
 }
 
-// Super-tile geometry of the envelope solve: TPS tiles per super-tile (the job's
-// comp_super frames rounded to whole tiles), SPC super-tiles per chunk, nch chunks.
-static void comp_geometry(const mm_job *j, int64_t G, int *TPS, int64_t *SPC, int64_t *nch) {
-    const int K = j->tiles_per_chunk;
-    *TPS = std::max(1, std::min((j->comp_super + j->tile / 2) / j->tile, P0_MAXL / 2));  // (a walk plus a warm-up super-tile)
-    *nch = (G + K - 1) / K;
-    *SPC = ((int64_t)K + *TPS - 1) / *TPS;
+// Geometry of the envelope solve (the C-ABI's mm_solve_geometry): TPS tiles per
+// super-tile (the job's comp_super frames rounded to whole tiles), columns per
+// chunk in whole blocks of 64 (comp_rms stores; a wave's columns lie in one
+// chunk), plane rows per tile and per column, and each chunk's own plane (32-bit
+// buffer offsets within it at any track length).
+static int solve_geometry(const mm_job *j, mm_solve_geom *g) {
+    const int K = j->tiles_per_chunk, T = j->tile;
+    if (K < 1 || T < 1 || j->frames_proc < 0) return MM_ERR_ARG;
+    const int64_t G = (j->frames_proc + T - 1) / T;
+    *g = mm_solve_geom{};
+    g->tps = std::max(1, std::min((j->comp_super + T / 2) / T, P0_MAXL / 2));  // (a walk plus a warm-up super-tile)
+    g->chunks = (G + K - 1) / K;
+    g->cols_per_chunk = (((int64_t)K + g->tps - 1) / g->tps + 63) / 64 * 64;
+    g->tile_rows = (T + WB - 1) / WB * WB;
+    g->rows = g->tps * g->tile_rows + WALK_PAD;
+    g->chunk_plane_bytes = (int64_t)g->rows * g->cols_per_chunk * 8;
+    g->plane_bytes = 3 * g->chunks * g->chunk_plane_bytes;
+    return g->chunk_plane_bytes < ((int64_t)1 << 31) ? MM_OK : MM_ERR_ARG;
 }
 
 // Control words of the whole chain, zeroed by ONE memset and read back by ONE
@@ -467,7 +470,6 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     const int64_t N = j->frames_proc;
     const int64_t G = c->G;
     const int64_t TG = (int64_t)T * std::max<int64_t>(G, 1);
-    const unsigned nb = blocks_for(std::max<int64_t>(G, 1), 256);
     CompArgs ca{};
     ca.N_proc = N;
     ca.G = G;
@@ -475,15 +477,19 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     ca.K = K;
     ca.ch = ch;
     ca.warmup = j->comp_warmup;
-    int64_t nchunks;
-    comp_geometry(j, G, &ca.TPS, &ca.SPC, &nchunks);
+    mm_solve_geom sg;
+    if (solve_geometry(j, &sg) != MM_OK)
+        return set_err(c, MM_ERR_ARG, "chunk of %d tiles too large for one envelope-solve plane", K);
+    const int64_t nchunks = sg.chunks;
+    ca.TPS = sg.tps;
+    ca.SPC = sg.cols_per_chunk;
     ca.GS = nchunks * ca.SPC;
     const int64_t NS = ca.GS;
     short2 *q2;
     RET(get_buf(c, "q2", TG, &q2));
     ca.q_out = q2;
     *q2_out = q2;
-    double *st, *ends, *luts, *tstc, *descc, *mmax, *mmaxc;
+    double *st, *ends, *luts, *tstc, *descc, *mmax, *mmaxc, *ced, *cedc;
     uint32_t *claims;
     RET(get_buf(c, "comp_start", (size_t)3 * NS, &st));
     RET(get_buf(c, "comp_end", (size_t)3 * NS, &ends));
@@ -493,6 +499,8 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     RET(get_buf(c, "comp_mmax", (size_t)3 * G, &mmax));
     RET(get_buf(c, "comp_tstc", (size_t)3 * NC, &tstc));
     RET(get_buf(c, "comp_mmaxc", (size_t)3 * NC, &mmaxc));
+    RET(get_buf(c, "comp_ced", (size_t)6 * G, &ced));
+    RET(get_buf(c, "comp_cedc", (size_t)6 * NC, &cedc));
     RET(get_buf(c, "comp_descc", (size_t)3 * DREC * NC, &descc));
     int32_t *ranks, *tls, *nacts;
     RET(get_buf(c, "comp_rank", (size_t)3 * G, &ranks));
@@ -503,15 +511,13 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     ca.walked = reinterpret_cast<unsigned long long *>(c->ctl + RB_WALKED);
     ca.trace = nullptr;
     if (getenv("MM_FIX_TRACE")) {  // diagnostics: per-walker sweep records, printed by evaluate_chain
-        RET(get_buf(c, "comp_trace", (size_t)16 * 3 * NS * 5, &ca.trace));
-        HIPCHK(c, hipMemsetAsync(ca.trace, 0, (size_t)16 * 3 * NS * 5 * sizeof(uint32_t), c->stream));
+        RET(get_buf(c, "comp_trace", (size_t)16 * 3 * NS * 4, &ca.trace));
+        HIPCHK(c, hipMemsetAsync(ca.trace, 0, (size_t)16 * 3 * NS * 4 * sizeof(uint32_t), c->stream));
     }
-    ca.RP = ca.TPS * T + WALK_PAD;
-    const int64_t ms_elems = (int64_t)ca.RP * ((NS + 63) / 64) * 64;  // column blocks of 64
-    if (ms_elems * 8 >= ((int64_t)1 << 32))
-        return set_err(c, MM_ERR_ARG, "track too long for one envelope solve (%lld frames): shard it by time",
-                       (long long)j->frames_proc);
-    ca.ms_bytes = (uint32_t)(ms_elems * 8);
+    ca.TP = sg.tile_rows;
+    ca.RP = sg.rows;
+    ca.chunk_elems = sg.chunk_plane_bytes / 8;  // SPC / 64 column blocks of 64 x RP
+    const int64_t ms_elems = ca.chunk_elems * nchunks;
     int32_t *cnt, *tot;
     RET(get_buf(c, "comp_cnt", (size_t)3 * G, &cnt));
     tot = reinterpret_cast<int32_t *>(c->ctl + RB_TOTALS);  // zeroed and read back with the control block
@@ -547,13 +553,15 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
         ca.nact[b] = nacts + (size_t)b * nchunks;
         ca.tl[b] = tls + (size_t)b * NC;
         ca.mmaxc[b] = mmaxc + (size_t)b * NC;
+        ca.ced[b] = ced + (size_t)2 * b * G;
+        ca.cedc[b] = cedc + (size_t)2 * b * NC;
         ca.tstc[b] = tstc + (size_t)b * NC;
         ca.descc[b] = descc + (size_t)b * DREC * NC;
         ca.start[b] = st + (size_t)b * NS;
         ca.end[b] = ends + (size_t)b * NS;
         ca.claim[b] = claims + (size_t)b * NS;
     }
-    RET(launch(c, "comp_rms", comp_rms_kernel, dim3(nb, 3), dim3(256), 0, ca));
+    RET(launch(c, "comp_rms", comp_rms_kernel, dim3(blocks_for(NS / 64 * ca.TPS, 4), 3), dim3(256), 0, ca));
     RET(launch(c, "comp_links", comp_links_kernel, dim3((unsigned)nchunks, 3), dim3(1024), 0, ca));
     if (ca.jumps)
         RET(launch(c, "comp_describe", comp_describe_kernel, dim3(blocks_for(G, DESC_BLOCK), 3), dim3(DESC_BLOCK), 0,
@@ -565,10 +573,9 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     c->comp_changed = changed;
     c->comp_iters = 0;
     c->comp_pending = 0;
-    c->comp_nb = nb;
     // as many as the last solve on this context needed (+ 1 spare): a stream of similar
-    // batches queues no idle sweeps and rarely resumes from the host
-    int sweeps = COMP_SWEEPS;
+    // jobs queues few idle sweeps and rarely resumes from the host
+    int sweeps = c->comp_queue > 0 ? c->comp_queue : COMP_SWEEPS;
     if (const char *e = getenv("MM_COMP_SWEEPS")) sweeps = std::max(1, std::min(16, atoi(e)));  // tests / tuning
     RET(comp_sweeps(c, sweeps));
     RET(comp_back(c));
@@ -591,8 +598,10 @@ static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
     const unsigned nblk = blocks_for(std::max<int64_t>(G, 1), tpb);
     int64_t nch = 0, spc = 0;
     if (j->multiband_on) {
-        int u;
-        comp_geometry(j, G, &u, &spc, &nch);
+        mm_solve_geom sg;
+        solve_geometry(j, &sg);  // (checked by stage_compress)
+        nch = sg.chunks;
+        spc = sg.cols_per_chunk;
     }
     RET(setup_control(c, nblk, nch, 3 * nch * spc));
 
@@ -1217,7 +1226,12 @@ static std::vector<BatchUnit> batch_units(const mm_job *J, int n) {
 // =================================================================== C-ABI
 extern "C" {
 
-int mm_version(void) { return 1; }
+int mm_version(void) { return MM_ABI_VERSION; }
+
+int mm_solve_geometry(const mm_job *j, mm_solve_geom *out) {
+    if (!j || !out) return MM_ERR_ARG;
+    return solve_geometry(j, out);
+}
 
 #ifndef MM_SOURCE_SHA
 #define MM_SOURCE_SHA "unknown"

@@ -31,16 +31,15 @@ EQ_PRESETS = {
 
 COMP_WARMUP = 0  # super-tiles of speculative warm-up walk before each one (none: the sweeps' jumps repair starts)
 COMP_MAX_ITERS = 100000
-# envelope solve unit in frames, at EVERY rate: 8 tiles of 125.  It is not scaled
-# with the rate: with 8 tiles per super-tile the 64 lanes (tiles) of a comp_rms wave
-# cover 8 whole super-tiles, so each M-plane store writes 8 runs of 64 B; at 96 kHz
-# the rate-scaled 17 tiles scattered them over ~64 lines (C5 21.2 -> 18.2 ms per
-# step).
-COMP_SUPER_FRAMES = 1000
+# envelope solve unit in frames, at EVERY rate: 4 tiles of 125.  Not scaled with the
+# rate (comp_rms maps a wave to one tile position of 64 super-tiles, so its M stores
+# are 512-byte runs at any length; shorter walks halve pass 0, and with the (max,+)
+# pass-0 guesses the sweeps barely lengthen: tools/study/envelope_model.c).
+COMP_SUPER_FRAMES = 500
 
 
 def comp_super_frames(rate: int, tile: int = design.DEFAULT_TILE) -> int:
-    """Super-tile length in frames: whole tiles (8 x 125 at every rate)."""
+    """Super-tile length in frames: whole tiles (4 x 125 at every rate)."""
     del rate  # (see COMP_SUPER_FRAMES)
     return max(1, int(round(COMP_SUPER_FRAMES / tile))) * tile
 

@@ -60,6 +60,15 @@ class MMResult(ctypes.Structure):
                 ("comp_jumped", ctypes.c_int64)]
 
 
+class MMSolveGeom(ctypes.Structure):
+    _fields_ = [("tps", ctypes.c_int32), ("tile_rows", ctypes.c_int32), ("rows", ctypes.c_int32),
+                ("_pad", ctypes.c_int32), ("cols_per_chunk", ctypes.c_int64), ("chunks", ctypes.c_int64),
+                ("chunk_plane_bytes", ctypes.c_int64), ("plane_bytes", ctypes.c_int64)]
+
+
+ABI_VERSION = 2  # MM_ABI_VERSION of include/mastering.h
+
+
 class MMWavInfo(ctypes.Structure):
     _fields_ = [("frames", ctypes.c_int64), ("data_offset", ctypes.c_int64), ("rate", ctypes.c_int32),
                 ("channels", ctypes.c_int32), ("format", ctypes.c_int32), ("bits", ctypes.c_int32)]
@@ -73,7 +82,8 @@ EXPORTS = ("mm_create", "mm_destroy", "mm_last_error", "mm_sync", "mm_version", 
            "mm_allreduce_sum_f64", "mm_allgather_f64", "mm_wav_probe", "mm_master_wav",
            "mm_op_pcm_to_float", "mm_op_saturation", "mm_op_stereo_width", "mm_op_quantize", "mm_op_soft_limiter",
            "mm_op_gain", "mm_op_sosfilt", "mm_op_loudness", "mm_op_multiband", "mm_master_batch",
-           "mm_op_saturation_legacy", "mm_op_soft_limiter_legacy", "mm_op_sosfilt_mix", "mm_op_compress_bands")
+           "mm_op_saturation_legacy", "mm_op_soft_limiter_legacy", "mm_op_sosfilt_mix", "mm_op_compress_bands",
+           "mm_solve_geometry")
 
 _lib = None
 _lock = threading.Lock()
@@ -135,11 +145,14 @@ def load():
             "mm_op_sosfilt_mix": ([vp, ctypes.c_int, vp, ctypes.c_int64, ctypes.c_int, P(MMIir), ctypes.c_double,
                                    ctypes.c_double, vp], ctypes.c_int),
             "mm_op_compress_bands": ([vp, P(MMJob), vp, vp, vp, vp], ctypes.c_int),
+            "mm_solve_geometry": ([P(MMJob), P(MMSolveGeom)], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             fn = getattr(lib, name)
             fn.argtypes = args
             fn.restype = res
+        if lib.mm_version() != ABI_VERSION:  # the structs above mirror one header version
+            raise RuntimeError(f"{LIB_PATH}: ABI version {lib.mm_version()}, this binding expects {ABI_VERSION}")
         _lib = lib
         return lib
 

@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared_functions():
         assert hasattr(lib, name), name
     assert sorted(native.EXPORTS) == declared_functions()
-    assert lib.mm_version() >= 1
+    assert lib.mm_version() == native.ABI_VERSION
 
 
 def test_library_was_built_from_these_sources():
@@ -54,6 +54,7 @@ def test_struct_layouts_match_c(tmp_path):
         "mm_band": [f[0] for f in native.MMBand._fields_],
         "mm_result": [f[0] for f in native.MMResult._fields_],
         "mm_wav_info": [f[0] for f in native.MMWavInfo._fields_],
+        "mm_solve_geom": [f[0] for f in native.MMSolveGeom._fields_],
     }
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "mastering.h"', "int main(void){"]
     for st, fl in fields.items():
@@ -66,7 +67,7 @@ def test_struct_layouts_match_c(tmp_path):
     subprocess.check_call(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)])
     got = dict(line.rsplit(" ", 1) for line in subprocess.check_output([str(exe)]).decode().splitlines())
     classes = {"mm_job": native.MMJob, "mm_iir": native.MMIir, "mm_band": native.MMBand,
-               "mm_result": native.MMResult, "mm_wav_info": native.MMWavInfo}
+               "mm_result": native.MMResult, "mm_wav_info": native.MMWavInfo, "mm_solve_geom": native.MMSolveGeom}
     for st, cls in classes.items():
         assert int(got[st]) == ctypes.sizeof(cls), st
         for f in fields[st]:
@@ -81,3 +82,31 @@ def test_product_path_fails_loudly_without_gpu():
     from mastering_amd import native
     with pytest.raises(RuntimeError):
         native.Context(0)
+
+
+@pytest.mark.parametrize("rate", [44100, 44056, 96000, 192000])
+def test_solve_geometry_up_to_2_31_frames(rate):
+    """The envelope solve's planning arithmetic (mm_solve_geometry, the function
+    stage C itself plans with) accepts every track length below 2^31 frames: each
+    chunk's M plane, walked through 32-bit buffer offsets, stays below 2^31 bytes
+    whatever the length (round 3 refused tracks above ~511 M frames)."""
+    from mastering_amd import design, engine, native
+    lib = native.load()
+    chunk = 30 * rate
+    tile = design.choose_tile(chunk)
+    prev = None
+    for frames in (1, chunk, 511_000_000, 576_000_000, 1_000_000_000, 2**31 - 1):
+        j = native.MMJob()
+        j.frames_in = j.frames_proc = frames
+        j.channels, j.rate, j.tile, j.tiles_per_chunk = 2, rate, tile, chunk // tile
+        j.comp_super = engine.comp_super_frames(rate, tile)
+        g = native.MMSolveGeom()
+        assert lib.mm_solve_geometry(ctypes.byref(j), ctypes.byref(g)) == 0, frames
+        assert g.chunks == -(-frames // chunk)
+        assert g.cols_per_chunk % 64 == 0 and g.cols_per_chunk * g.tps >= chunk // tile
+        assert g.tile_rows >= tile and g.tile_rows % 25 == 0
+        assert 0 < g.chunk_plane_bytes < 2**31
+        assert g.plane_bytes == 3 * g.chunks * g.chunk_plane_bytes
+        if prev is not None:  # per-chunk geometry does not depend on the length
+            assert (g.tps, g.rows, g.cols_per_chunk, g.chunk_plane_bytes) == prev
+        prev = (g.tps, g.rows, g.cols_per_chunk, g.chunk_plane_bytes)

@@ -25,12 +25,14 @@ def rms_diff(a, b):
 
 
 # Identical int16 output samples, tied to what is measured (round 3, `pytest -m gpu`
-# summary): 99.960-99.992 % on every full-chain case but loud_sat100 (99.871 %).  The
-# differences come from numpy's float32 tanh (not correctly rounded),
-# carried through the compressor; with the exciter off the pre-gain mix is 100 %
-# identical (test_mix_bit_exact_without_tanh).  The floor allows twice the worst
-# measured mismatch rate, so a regression from 99.98 % to 99.9 % fails.
-MIN_EXACT = 0.9992
+# summary, profiles/r03_final_gpu_pytest.log): 99.9457-99.992 % on every full-chain
+# case but loud_sat100 (99.871 %, its own floor), the lowest being
+# test_batch_device_resident at 44.1 kHz (0.9994570).  The differences come from
+# numpy's float32 tanh (not correctly rounded), carried through the
+# compressor; with the exciter off the pre-gain mix is 100 % identical
+# (test_mix_bit_exact_without_tanh).  The floor allows twice the worst measured
+# mismatch rate (2 x 5.43e-4), so a regression from 99.95 % to 99.8 % fails.
+MIN_EXACT = 0.9989
 
 
 def _check(out, info, ref, L, min_exact=MIN_EXACT):
@@ -266,3 +268,18 @@ def test_batch_mixed_settings_units(oracle):
         ref, L = oracle.master(pcm, rate, st, return_loudness=True)
         assert res[t].frames_out == jobs[t].frames_proc
         _check(outs[t].cpu().numpy(), {"loudness": res[t].loudness}, ref, L)
+
+
+def test_multiband_at_rate_without_25_frame_tiles(oracle):
+    """44056 Hz: no tile length in [64, 512] that divides the 30 s chunk is a
+    multiple of the walkers' 25-row load blocks (choose_tile picks 240): the
+    M plane pads each tile to whole blocks with identity rows (round 3 refused
+    this rate with multiband on)."""
+    from mastering_amd import design, master_pcm
+    from mastering_amd.synth import pink_noise_pcm16
+    rate = 44056
+    assert design.choose_tile(30 * rate) % 25 != 0
+    pcm = pink_noise_pcm16(40 * rate, rate, 2, 21)
+    out, info = master_pcm(pcm, rate, P_HOT)
+    ref, L = oracle.master(pcm, rate, P_HOT, return_loudness=True)
+    _check(out, info, ref, L)
