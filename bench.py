@@ -62,6 +62,7 @@ import numpy as np  # noqa: E402
 METRIC = "stereo frames/sec through full mastering chain, 44.1 kHz f32; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 CHAIN_BYTES_PER_FRAME = 16  # f32 L,R in + f32 L,R out
+PROFILE_ROUND = "r04"  # profiles/<round>_<workload>_pmc_summary.json carry the PMC traffic
 P_FULL = {"bass_boost": 4.0, "mid_cut": 3.0, "presence_boost": 1.0, "treble_boost": 3.0,
           "saturation": 30, "width": 1.3, "multiband": True, "lufs": -14.0}
 P_HOT = dict(P_FULL, low_thresh=-16.0, mid_thresh=-21.0, high_thresh=-27.0)
@@ -101,9 +102,12 @@ def source_sha() -> str:
     return h.hexdigest()[:16]
 
 
-def algorithmic_bytes(kernel, n, g, active, walked_per_launch):
-    """Minimum HBM bytes one launch must move for its own inputs/outputs (stereo,
-    n frames, g tiles, `active` compressor frames over the 3 bands)."""
+def intermediate_bytes(kernel, n, g, active, walked_per_launch):
+    """HBM bytes one launch moves for its own inputs/outputs in this design (stereo,
+    n frames, g tiles, `active` compressor frames over the 3 bands), intermediates
+    included: the kernel's own data-flow floor, NOT SURVEY §8(d)'s algorithmic
+    bytes (16 B per stereo frame for the whole chain, which the headline and the
+    dominant kernel's `frac` use)."""
     table = {
         "eq": 8 * n + 4 * n,                  # f32 L,R in; int16 pair q1 out
         "pre_pointwise": 8 * n + 4 * n,
@@ -394,13 +398,16 @@ def main():
         n_frames = run.frames_step
         g_tiles = sum(j.G for j in run.jobs)
         walked_per_launch = walked / max(launches, 1) if dom == "comp_fix" else 0
-        bpl = algorithmic_bytes(dom, n_frames, g_tiles, active, walked_per_launch)
-        k_achieved = bpl / avg_s / 1e9 if bpl is not None else None
+        ibl = intermediate_bytes(dom, n_frames, g_tiles, active, walked_per_launch)
+        # 16 B per stereo frame; a launch processes the step's frames over
+        # its launches per step (a kernel launched once per step: every frame)
+        bpl = CHAIN_BYTES_PER_FRAME * n_frames / max(launches, 1)
+        k_achieved = bpl / avg_s / 1e9
         chain_gbs = CHAIN_BYTES_PER_FRAME * n_frames / (ms_step / 1e3) / 1e9
         # PMC traffic and SQ shares, only from a profile of these exact sources
         sha = source_sha()
         default_params = WORKLOADS[args.workload].get("params", "full")
-        tag = args.profile_tag or f"r03_{args.workload}" + ("" if args.params == default_params else args.params)
+        tag = args.profile_tag or f"{PROFILE_ROUND}_{args.workload}" + ("" if args.params == default_params else args.params)
         prof, prof_path = profile_summary(tag)
         traffic = limiter = dom_traffic = None
         valu = None
@@ -433,8 +440,15 @@ def main():
                          "scope": "whole chain: 16 B per stereo frame over ms_per_step",
                          "profile": prof_note, "source_sha": sha,
                          "dominant_kernel": {"name": dom, "achieved": k_achieved,
-                                             "frac": k_achieved / HBM_PEAK_GBS if k_achieved else None,
-                                             "algorithmic_bytes_per_launch": bpl, "avg_launch_ms": avg_s * 1e3,
+                                             "frac": k_achieved / HBM_PEAK_GBS,
+                                             "algorithmic_bytes_per_launch": bpl,
+                                             "scope": "16 B per stereo frame (SURVEY §8(d)) x frames per launch "
+                                                      "(the step's frames / launches per step), over the "
+                                                      "kernel's event-timed average launch",
+                                             "intermediate_bytes_per_launch": ibl,
+                                             "intermediate_frac": (ibl / avg_s / 1e9 / HBM_PEAK_GBS
+                                                                   if ibl is not None else None),
+                                             "avg_launch_ms": avg_s * 1e3,
                                              "launches_per_step": launches, "traffic": dom_traffic},
                          "valu_ceiling": valu},
             "chain": {"device_ms_per_step": sum(v[0] for v in per.values()),

@@ -152,7 +152,8 @@ struct CompArgs {
     double *mmax[3];           // per tile: largest M
     double *ced[3];            // per tile: (max,+) release summary {c, D} (double2; comp_rms)
     int32_t *total[3];         // per chunk: active frames (statistics)
-    int32_t *rank[3];          // per tile: active tiles before it in its chunk (comp_links)
+    int32_t *cbtot[3];         // per column block: active tiles (comp_rms; zeroed per chain)
+    int32_t *rank[3];          // per tile: active tiles before it in its chunk (comp_describe)
     int32_t *nact[3];          // per chunk: active tiles
     // per active tile at compact index ci = chunk * K + rank:
     int32_t *tl[3];            // the tile
@@ -164,6 +165,9 @@ struct CompArgs {
     double *end[3];            // per-super-tile end state (one buffer; sweeps hand ends over with sc1 accesses)
     uint32_t *claim[3];        // per super-tile: the last sweep stamp that claimed it (zeroed per chain)
     int jumps;                 // release jumps enabled (MM_COMP_NOJUMP=1 disables them: diagnostics)
+    int sjump;                 // super-tile jumps enabled (MM_COMP_NOSJUMP=1 disables them: diagnostics)
+    double *sdesc[3];          // per super-tile: composed release-jump record (compressor.hip compose_super)
+    int32_t *se0[3];           // per super-tile: binade of its largest M (SJ_NONE: no record)
     uint32_t stamp;            // this sweep's stamp (> every earlier one of the chain)
     int heads;                 // 0: Jacobi sweep (every stale super-tile walks); 1: run heads only
     unsigned int *changed;

@@ -19,13 +19,13 @@
 //                into a super-tile-major M plane (column blocks of 64, so 64
 //                walkers read 512 contiguous bytes per step), the tile's active
 //                count and largest M;
-//  2. comp_links per (chunk, band): ranks and lists the active tiles;
+//  2. comp_describe per column block: ranks and lists the active tiles (comp_links
+//                until round 3) and
 //  3. comp_pass0 walker lanes (one per super-tile, a wave in lockstep) walk from a
 //                guess (the (max,+) release envelope of the preceding active
 //                tiles; exactly 0 at the chunk's first active tile), storing every
-//                tile's entry state and the end;
-//                comp_describe (one lane per active tile, launched before it)
-//                records the exact effect of the tile's T release steps on any
+//                tile's entry state and the end; comp_describe (before it) records
+//                per active tile the exact effect of its T release steps on any
 //                state of the four binades above its largest M (release jumps);
 //  4. comp_fix   sweeps: a super-tile whose start differs from its predecessor's
 //                end re-walks from it tile by tile — jumped over pure-release
@@ -251,6 +251,11 @@ __global__ void __launch_bounds__(256) comp_rms_kernel(CompArgs a) {
     for (int i = max(len, 0); i < a.TP; ++i, e += GS32) Mo[e] = 0.0;
     a.cnt[b][g] = active;
     a.mmax[b][g] = lut[rmx];
+    {  // active tiles of the column block (comp_describe ranks the chunk's active tiles from them)
+        const int na = (int)__popcll(__ballot(active != 0));
+        if (__lane_id() == __builtin_amdgcn_readfirstlane(__lane_id()) && na)
+            atomicAdd(a.cbtot[b] + (sc >> 6), na);
+    }
     reinterpret_cast<double2 *>(a.ced[b])[g] = make_double2(ce, De);
     // per-chunk active count (statistics): one atomic per wave when all 64 lanes
     // are live (lanes past the chunk's tiles or G exited above; the wave's tiles
@@ -326,7 +331,7 @@ __device__ __forceinline__ double lean_step(double att, double m, double inc, do
 
 // ---- envelope walks over the M plane ------------------------------------------
 // The solve runs over each chunk's ACTIVE tiles (an inactive tile holds the
-// state): comp_links ranks them (rank[g] = active tiles before tile g in its
+// state): comp_describe ranks them (rank[g] = active tiles before tile g in its
 // chunk, compact index ci = chunk * K + rank), and super-tile j of chunk c is
 // the active tiles of ranks [j*TPS, min((j+1)*TPS, nact[c])) — empty past the
 // chunk's active tiles.  Its state on entry, the tiles' entry states (tstc) and
@@ -557,64 +562,68 @@ struct Describer {
     }
 };
 
-// 2. links.  grid (chunks, 3), 1024 threads: ranks the chunk's active tiles
-// (rank[g] for every tile: active tiles before it), lists them (tl[ci] = tile,
-// mmaxc[ci] = its largest M) and counts them (nact[c]).
-__global__ void __launch_bounds__(1024) comp_links_kernel(CompArgs a) {
-    __shared__ int32_t sums[1024];
-    const int b = blockIdx.y;
-    const int64_t c = blockIdx.x, g0 = c * a.K;
-    const int n = (int)min((int64_t)a.K, a.G - g0);
-    const int per = (n + 1023) / 1024;
-    const int tid = threadIdx.x;
-    const int i0 = min(tid * per, n), i1 = min(i0 + per, n);
-    int32_t cntl = 0;
-    for (int i = i0; i < i1; ++i) cntl += a.cnt[b][g0 + i] != 0 ? 1 : 0;
-    sums[tid] = cntl;
-    __syncthreads();
-    int32_t v = cntl;
-    for (int d = 1; d < 1024; d <<= 1) {
-        const int32_t o = tid >= d ? sums[tid - d] : 0;
-        __syncthreads();
-        v += o;
-        sums[tid] = v;
-        __syncthreads();
-    }
-    int32_t r = v - cntl;  // exclusive
-    for (int i = i0; i < i1; ++i) {
-        const int64_t g = g0 + i;
-        a.rank[b][g] = r;
-        if (a.cnt[b][g] != 0) {
-            a.tl[b][g0 + r] = (int32_t)g;
-            a.mmaxc[b][g0 + r] = a.mmax[b][g];
-            reinterpret_cast<double2 *>(a.cedc[b])[g0 + r] = reinterpret_cast<const double2 *>(a.ced[b])[g];
-            ++r;
-        }
-    }
-    if (tid == 1023) a.nact[b][c] = v;
-}
-
-// 3a. describers.  grid: (ceil(G/DESC_BLOCK), 3), lane = tile: an active tile's
-// release-jump record.  Its own launch (before pass 0), so its waves are not held to
-// the walkers' register budget: at ~100 VGPRs 4-5 describer waves share a SIMD,
-// where inside pass 0 they ran 2 per SIMD behind the walkers and set pass 0's time.
+// 2. links + describers, ONE launch.  grid: (column blocks, 3), a block of
+// 64 * TPS threads = one column block (64 super-tiles x TPS tiles = 64 TPS
+// consecutive tiles of one chunk), lanes mapped to tiles as in comp_rms (wave k:
+// tile position k of the 64 columns), so the describers' M loads are 512-byte runs.
+//  * links: ranks the chunk's active tiles (rank[g] = active tiles before g in its
+//    chunk: the counts comp_rms left per column block for the blocks before this
+//    one, plus a scan over the block's tiles in tile order), lists them at compact
+//    index ci = chunk * K + rank (tl = the tile, mmaxc = its largest M, cedc = its
+//    (max,+) summary) and counts them (nact[c], by the chunk's last block);
+//  * describers: an active tile's release-jump record (Describer).
+// (Round 3 ran the links as one 1024-thread block per chunk and band: 30 blocks
+// for a 5-min track, 26 us of latency before the describers' own launch.)
 #ifndef MM_DESC_NB
 #define MM_DESC_NB 1
 #endif
-constexpr int DESC_BLOCK = 256;
+constexpr int DESC_MAX_TPS = 16;  // block = 64 * TPS <= 1024 threads
 
-// Lanes map to tiles as in comp_rms (a wave: one tile position of 64 columns of one
-// chunk), so every step's loads are one 512-byte run.
-__global__ void __launch_bounds__(DESC_BLOCK) comp_describe_kernel(CompArgs a) {
+__global__ void __launch_bounds__(64 * DESC_MAX_TPS) comp_describe_kernel(CompArgs a) {
+    __shared__ int32_t wsum[DESC_MAX_TPS], base_s;
+    __shared__ uint8_t flag[64 * DESC_MAX_TPS];
+    __shared__ int32_t pre[64 * DESC_MAX_TPS];
     const int b = blockIdx.y;
-    const int64_t wv = (int64_t)blockIdx.x * (DESC_BLOCK / 64) + (threadIdx.x >> 6);
-    const int kc = (int)(wv % a.TPS);
-    const int64_t sc = (wv / a.TPS) * 64 + (threadIdx.x & 63);
+    const int TPS = a.TPS, NT = 64 * TPS;
+    const int kc = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int64_t cb = blockIdx.x;  // column block
+    const int64_t sc = cb * 64 + l;
     const int64_t cc = sc / a.SPC;
-    const int64_t jt = (sc - cc * a.SPC) * a.TPS + kc;
+    const int64_t cbl = (sc - cc * a.SPC) >> 6;  // column block within the chunk
+    const int64_t jt = (sc - cc * a.SPC) * TPS + kc;
     const int64_t g = cc * a.K + jt;
-    const bool live = jt < a.K && g < a.G && a.cnt[b][min(g, a.G - 1)] != 0;
-    if (__all(!live)) return;
+    const bool valid = jt < a.K && g < a.G;
+    const bool live = valid && a.cnt[b][g] != 0;
+    // tile order within the block: tile jt = (column block base) + l * TPS + kc
+    flag[l * TPS + kc] = live ? 1 : 0;
+    if (threadIdx.x == 0) {  // active tiles of the chunk's earlier column blocks (comp_rms counts)
+        int32_t acc = 0;
+        const int32_t *ct = a.cbtot[b] + cc * (a.SPC >> 6);
+        for (int64_t q = 0; q < cbl; ++q) acc += ct[q];
+        base_s = acc;
+    }
+    __syncthreads();
+    // exclusive scan of the flags in tile order: thread t takes entry t
+    const int t = threadIdx.x;
+    const bool f = flag[t] != 0;
+    const uint64_t bal = __ballot(f);
+    const int wp = (int)__popcll(bal & ((1ull << (t & 63)) - 1ull));
+    if ((t & 63) == 0) wsum[t >> 6] = (int32_t)__popcll(bal);
+    __syncthreads();
+    int32_t woff = base_s;
+    for (int w = 0; w < (t >> 6); ++w) woff += wsum[w];
+    pre[t] = woff + wp;
+    if (t == NT - 1 && cbl == (a.SPC >> 6) - 1) a.nact[b][cc] = woff + wp + (f ? 1 : 0);  // the chunk's last block
+    __syncthreads();
+    const int32_t r = pre[l * TPS + kc];
+    const int64_t ci = cc * a.K + r;
+    if (valid) a.rank[b][g] = r;
+    if (live) {
+        a.tl[b][ci] = (int32_t)g;
+        a.mmaxc[b][ci] = a.mmax[b][g];
+        reinterpret_cast<double2 *>(a.cedc[b])[ci] = reinterpret_cast<const double2 *>(a.ced[b])[g];
+    }
+    if (!a.jumps || __all(!live)) return;
     const int64_t gc = live ? g : cc * a.K;  // (dead lanes: the chunk's first tile)
     Describer d;
     d.bs = band_step(a, b);
@@ -622,7 +631,78 @@ __global__ void __launch_bounds__(DESC_BLOCK) comp_describe_kernel(CompArgs a) {
     d.e0 = mx > 0.0 ? binade(mx) : 0;
     const uint32_t off = tile_off(a, gc);
     stream_col<true, MM_DESC_NB>(plane(a, b, cc), [&](int) { return off; }, 1, a.TP, d);
-    if (live) d.store(a.descc[b] + (cc * a.K + a.rank[b][gc]) * DREC);
+    if (live) d.store(a.descc[b] + ci * DREC);
+}
+
+// ---- super-tile release jumps --------------------------------------------------
+// A full super-tile (SJ_TPS active tiles) gets a record composed from its tiles'
+// release-jump records (pass 0 writes it): for a state a of binade e = e0s + kb
+// (e0s: binade of the super-tile's largest M, kb < JB) and mantissa parity p, the
+// SJ_TPS tile jumps are taken one after another iff a > L[kb][p] and a - Q[SJ_TPS]
+// stays in binade e with a nonzero mantissa; Q[t] is the exact offset after t tiles
+// (so the tiles' entry states are a - Q[t]).  Exactness: tile t's jump from
+// a_t = a - Q[t] needs a_t - q_t > mx_t (L >= mx_t + Q[t+1], rounded up), x_t in
+// binade e with a nonzero mantissa (x_t >= the final state >= 2^e + u, x_t < a <
+// 2^(e+1)), and tile t's record to cover binade e with the parity of a_t (tracked:
+// a_t - q_t flips it iff q_t / u is odd).  L = NaN: some tile's record does not
+// cover (e, p), or the offsets leave the binade.  The fix-up walkers cross a
+// release stretch a super-tile per jump (the long sweep chains are jump chains:
+// tools/study/envelope_model.c), with the next record prefetched.
+constexpr int SJ_TPS = 4;               // tiles per super-tile with records
+constexpr int SJ_ENT = SJ_TPS + 1;      // doubles per (kb, p) entry: L, Q[1..SJ_TPS]
+constexpr int SREC = 2 * JB * SJ_ENT;   // doubles per super-tile record
+constexpr int SJ_NONE = -100000;        // se0 of a super-tile without a record
+
+__device__ __forceinline__ double next_up(double x) {
+    return x > 0.0 ? __longlong_as_double(__double_as_longlong(x) + 1) : x;
+}
+
+// pass 0, lane = a full super-tile s with its first tile at compact index ci0
+__device__ void compose_super(const CompArgs &a, int b, int64_t s, int64_t ci0) {
+    double mxs = 0.0;
+#pragma unroll
+    for (int t = 0; t < SJ_TPS; ++t) mxs = fmax(mxs, a.mmaxc[b][ci0 + t]);
+    const int e0s = binade(mxs);
+    double Q[2 * JB], L[2 * JB];
+    int par[2 * JB];
+    bool ok[2 * JB];
+#pragma unroll
+    for (int k = 0; k < 2 * JB; ++k) {
+        Q[k] = 0.0;
+        L[k] = 0.0;
+        par[k] = k & 1;
+        ok[k] = true;
+    }
+    double *rec = a.sdesc[b] + s * SREC;
+    for (int t = 0; t < SJ_TPS; ++t) {
+        const double mx = a.mmaxc[b][ci0 + t];
+        const int e0t = binade(mx);
+        double q[2 * JB];
+        const double2 *r = reinterpret_cast<const double2 *>(a.descc[b] + (ci0 + t) * DREC);
+#pragma unroll
+        for (int k = 0; k < JB; ++k) {
+            const double2 v = r[k];
+            q[2 * k] = v.x;
+            q[2 * k + 1] = v.y;
+        }
+#pragma unroll
+        for (int k = 0; k < 2 * JB; ++k) {
+            const int e = e0s + k / 2, kt = e - e0t;
+            const int idx = 2 * min(max(kt, 0), JB - 1) + par[k];
+            double qv = q[0];
+#pragma unroll
+            for (int j = 1; j < 2 * JB; ++j) qv = idx == j ? q[j] : qv;
+            ok[k] = ok[k] && kt >= 0 && kt < JB && qv == qv;
+            Q[k] += ok[k] ? qv : 0.0;
+            ok[k] = ok[k] && Q[k] < ldexp(1.0, e);
+            if (ok[k]) par[k] ^= (int)((int64_t)ldexp(qv, 52 - e) & 1);  // qv / u, an exact integer
+            L[k] = fmax(L[k], next_up(mx + Q[k]));
+            rec[k * SJ_ENT + 1 + t] = Q[k];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 2 * JB; ++k) rec[k * SJ_ENT] = ok[k] ? L[k] : __longlong_as_double(0x7ff8000000000000ll);
+    a.se0[b][s] = e0s;
 }
 
 // 3b. speculative pass.  grid: (ceil(GS/64), 3) of 64-lane blocks, lane =
@@ -675,6 +755,10 @@ __global__ void __launch_bounds__(PASS0_BLOCK) comp_pass0_kernel(CompArgs a) {
             const double2 v = cd[i];
             att = fmax(v.x, att - v.y);
         }
+    }
+    if (a.sjump) {  // the super-tile's release-jump record (the sweeps' super jumps)
+        if (live && st.ntiles == SJ_TPS && a.TPS == SJ_TPS) compose_super(a, b, s, st.ci0);
+        else if (s < a.GS) a.se0[b][s] = SJ_NONE;
     }
     Walker<true> w;
     w.att = att;
@@ -776,11 +860,59 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
     };
     int64_t cur = s;
     bool nx_claimed = a.heads && !st.last ? comp_claim(a, b, cur + 1) : false;
-    TileMeta ring[FIX_AHEAD];
+    // super jumps (full super-tiles of SJ_TPS tiles): the record entries (both
+    // parities) of the next super-tile are loaded one super-tile ahead for the
+    // binade the state has now (a release stretch stays in its binade for many
+    // super-tiles), its se0 two ahead, so a stretch is crossed without waiting on
+    // memory; a binade change costs one dependent load.
+    const bool sj = a.sjump && a.jumps && a.TPS == SJ_TPS;
+    const double *srec = a.sdesc[b];
+    const int32_t *se0 = a.se0[b];
+    const int64_t slast = (s / a.SPC) * a.SPC + a.SPC - 1;  // (clamp for the prefetches: the chunk's columns)
+    int e0_c = SJ_NONE, e0_n = SJ_NONE;   // se0 of cur, cur + 1
+    int kb_c = -1, kb_n = -1;             // binade offsets the prefetched entries are for
+    double old_c = 0.0, old_n = 0.0;      // stored entry states of cur's, cur + 1's first tile
+    double ec[2][SJ_ENT], en[2][SJ_ENT];  // entries (parity 0, 1) of cur, cur + 1
+    auto ld_ent = [&](int64_t sx, int kb, double (&e)[2][SJ_ENT]) __attribute__((always_inline)) {
+        const double *r = srec + min(sx, slast) * SREC + 2 * min(max(kb, 0), JB - 1) * SJ_ENT;
 #pragma unroll
-    for (int k = 0; k < FIX_AHEAD; ++k) ring[k] = ld(st.ci0 + k);
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+            for (int j = 0; j < SJ_ENT; ++j) e[q][j] = r[q * SJ_ENT + j];
+    };
+    if (sj) {
+        e0_c = se0[cur];
+        e0_n = se0[min(cur + 1, slast)];
+        old_c = tst[st.ci0];
+        kb_c = binade(att) - e0_c;
+        ld_ent(cur, kb_c, ec);
+    }
+    // advance the prefetch pipeline to super-tile cur (its predecessor's data shifts in)
+    auto sj_advance = [&]() __attribute__((always_inline)) {
+        e0_c = e0_n;
+        kb_c = kb_n;
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+            for (int j = 0; j < SJ_ENT; ++j) ec[q][j] = en[q][j];
+        e0_n = se0[min(cur + 1, slast)];
+        old_c = old_n;
+    };
+    auto sj_prefetch = [&]() __attribute__((always_inline)) {  // cur + 1: first stored state, entries
+        old_n = tst[min(st.ci0 + st.ntiles, cend - 1)];
+        kb_n = binade(att) - e0_n;
+        ld_ent(cur + 1, kb_n, en);
+    };
+    if (sj) sj_prefetch();
+    TileMeta ring[FIX_AHEAD];
+    bool ring_ok = !sj;  // the ring holds tiles ci .. ci + FIX_AHEAD - 1
+    if (ring_ok) {
+#pragma unroll
+        for (int k = 0; k < FIX_AHEAD; ++k) ring[k] = ld(st.ci0 + k);
+    }
     a.start[b][cur] = att;
     int64_t ci = st.ci0, ce = st.ci0 + st.ntiles;  // position, end of cur
+    bool sj_try = sj && st.ntiles == SJ_TPS;       // at the start of a full super-tile
     // after tile ci: the end of cur publishes its end and continues into the
     // successor if it is (or can be) claimed; false: the walk ends
     auto next = [&]() __attribute__((always_inline)) -> bool {
@@ -795,6 +927,11 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
         ce = st.ci0 + st.ntiles;
         nx_claimed = a.heads && !st.last ? comp_claim(a, b, cur + 1) : false;
         ++n_vis;
+        if (sj) {
+            sj_advance();
+            sj_prefetch();
+            sj_try = st.ntiles == SJ_TPS;
+        }
         return true;
     };
     // Lanes run through coalescence checks and jumps on their own until each needs
@@ -804,6 +941,44 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
     bool run = true, walk = false;
     for (;;) {
         while (run && !walk) {
+            if (sj_try) {  // a whole super-tile in one jump?
+                sj_try = false;
+                const double old0 = ring_ok ? ring[0].old : old_c;
+                if (__double_as_longlong(old0) == __double_as_longlong(att)) {  // coalesced
+                    run = false;
+                    break;
+                }
+                constexpr uint64_t MANT = (1ull << 52) - 1;
+                const uint64_t ab = (uint64_t)__double_as_longlong(att);
+                const int kb = (int)(ab >> 52) - 1023 - e0_c;
+                if (att > 0.0 && kb >= 0 && kb < JB) {
+                    if (kb != kb_c) {  // the state left the prefetched binade
+                        kb_c = kb;
+                        ld_ent(cur, kb, ec);
+                    }
+                    const int par = (int)(ab & 1);
+                    const double L = par ? ec[1][0] : ec[0][0];
+                    const double Qt = par ? ec[1][SJ_TPS] : ec[0][SJ_TPS];
+                    const double x = att - Qt;
+                    const uint64_t xb = (uint64_t)__double_as_longlong(x);
+                    if (att > L && (xb >> 52) == (ab >> 52) && (xb & MANT) != 0) {
+                        tst[ci] = att;
+#pragma unroll
+                        for (int t = 1; t < SJ_TPS; ++t) tst[ci + t] = att - (par ? ec[1][t] : ec[0][t]);
+                        att = x;
+                        jumped += (int64_t)SJ_TPS * T;
+                        ci += SJ_TPS - 1;
+                        ring_ok = false;
+                        run = next();
+                        continue;
+                    }
+                }
+            }
+            if (!ring_ok) {  // tile by tile from ci
+#pragma unroll
+                for (int k = 0; k < FIX_AHEAD; ++k) ring[k] = ld(ci + k);
+                ring_ok = true;
+            }
             m = ring[0];
 #pragma unroll
             for (int k = 0; k + 1 < FIX_AHEAD; ++k) ring[k] = ring[k + 1];

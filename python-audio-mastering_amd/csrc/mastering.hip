@@ -372,6 +372,12 @@ static int evaluate_chain(mm_ctx *c, bool *converged) {
         const int64_t NS = c->ca.GS;
         std::vector<uint32_t> tr((size_t)16 * 3 * NS * 4);
         HIPCHK(c, hipMemcpy(tr.data(), c->ca.trace, tr.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        if (const char *path = getenv("MM_FIX_TRACE_DUMP")) {  // every walker record: [sweep][band][super-tile][4]
+            if (FILE *f = fopen(path, "wb")) {
+                fwrite(tr.data(), sizeof(uint32_t), tr.size(), f);
+                fclose(f);
+            }
+        }
         for (int k = 0; k < 16; ++k) {
             std::vector<std::pair<uint32_t, int64_t>> v;
             int64_t nw = 0;
@@ -426,7 +432,7 @@ static int solve_geometry(const mm_job *j, mm_solve_geom *g) {
     if (K < 1 || T < 1 || j->frames_proc < 0) return MM_ERR_ARG;
     const int64_t G = (j->frames_proc + T - 1) / T;
     *g = mm_solve_geom{};
-    g->tps = std::max(1, std::min((j->comp_super + T / 2) / T, P0_MAXL / 2));  // (a walk plus a warm-up super-tile)
+    g->tps = std::max(1, std::min((j->comp_super + T / 2) / T, DESC_MAX_TPS));  // (comp_describe: 64 TPS threads)
     g->chunks = (G + K - 1) / K;
     g->cols_per_chunk = (((int64_t)K + g->tps - 1) / g->tps + 63) / 64 * 64;
     g->tile_rows = (T + WB - 1) / WB * WB;
@@ -493,7 +499,7 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     uint32_t *claims;
     RET(get_buf(c, "comp_start", (size_t)3 * NS, &st));
     RET(get_buf(c, "comp_end", (size_t)3 * NS, &ends));
-    claims = c->ctl_claims;  // zeroed with the control block (sized by stage_front)
+    claims = c->ctl_claims;  // zeroed with the control block (sized by stage_front: claims, then cbtot)
     RET(get_buf(c, "comp_lut", (size_t)3 * 32769, &luts));
     const int64_t NC = nchunks * K;  // compact indices
     RET(get_buf(c, "comp_mmax", (size_t)3 * G, &mmax));
@@ -507,6 +513,11 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     RET(get_buf(c, "comp_tl", (size_t)3 * NC, &tls));
     RET(get_buf(c, "comp_nact", (size_t)3 * nchunks, &nacts));
     ca.jumps = getenv("MM_COMP_NOJUMP") ? 0 : 1;  // diagnostics: results must not change
+    ca.sjump = ca.jumps && !getenv("MM_COMP_NOSJUMP") && ca.TPS == SJ_TPS ? 1 : 0;
+    double *sdesc;
+    int32_t *se0s;
+    RET(get_buf(c, "comp_sdesc", ca.sjump ? (size_t)3 * NS * SREC : 1, &sdesc));
+    RET(get_buf(c, "comp_se0", ca.sjump ? (size_t)3 * NS : 1, &se0s));
     unsigned int *changed = c->comp_changed;  // zeroed with the chain's control words
     ca.walked = reinterpret_cast<unsigned long long *>(c->ctl + RB_WALKED);
     ca.trace = nullptr;
@@ -560,12 +571,12 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
         ca.start[b] = st + (size_t)b * NS;
         ca.end[b] = ends + (size_t)b * NS;
         ca.claim[b] = claims + (size_t)b * NS;
+        ca.sdesc[b] = ca.sjump ? sdesc + (size_t)b * NS * SREC : nullptr;
+        ca.se0[b] = ca.sjump ? se0s + (size_t)b * NS : nullptr;
+        ca.cbtot[b] = reinterpret_cast<int32_t *>(claims + (size_t)3 * NS) + (size_t)b * (NS / 64);
     }
     RET(launch(c, "comp_rms", comp_rms_kernel, dim3(blocks_for(NS / 64 * ca.TPS, 4), 3), dim3(256), 0, ca));
-    RET(launch(c, "comp_links", comp_links_kernel, dim3((unsigned)nchunks, 3), dim3(1024), 0, ca));
-    if (ca.jumps)
-        RET(launch(c, "comp_describe", comp_describe_kernel, dim3(blocks_for(G, DESC_BLOCK), 3), dim3(DESC_BLOCK), 0,
-                   ca));
+    RET(launch(c, "comp_describe", comp_describe_kernel, dim3((unsigned)(NS / 64), 3), dim3(64 * ca.TPS), 0, ca));
     RET(launch(c, "comp_pass0", comp_pass0_kernel, dim3(blocks_for(NS, PASS0_BLOCK), 3), dim3(PASS0_BLOCK), 0, ca));
     c->comp_on = true;
     c->ca = ca;
@@ -603,7 +614,7 @@ static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
         nch = sg.chunks;
         spc = sg.cols_per_chunk;
     }
-    RET(setup_control(c, nblk, nch, 3 * nch * spc));
+    RET(setup_control(c, nblk, nch, 3 * nch * spc + 3 * nch * spc / 64));  // claim stamps, column-block counts
 
     EqArgs ea{};
     ea.in = j->in_kind == MM_IN_I16 ? nullptr : static_cast<const float *>(d_in);

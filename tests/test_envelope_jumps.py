@@ -123,3 +123,84 @@ def test_release_jumps_are_exact():
                     y = _step(y, m, A, R)
                 assert x == y, (s0, att, x, y)
     assert jumps > 0.3 * checked, (jumps, checked)  # the jump conditions are not vacuous
+
+
+SJ_TPS = 4  # tiles per super-tile with a composed record (== csrc/compressor.hip SJ_TPS)
+
+
+def _binade(x):
+    return (_bits(x) >> 52) - 1023
+
+
+def _next_up(x):
+    return math.nextafter(x, math.inf) if x > 0.0 else x
+
+
+def _compose_super(descs):
+    """compose_super: (e0s, entries[2 JB] of (L, [Q1..Q_TPS])) from SJ_TPS tile descriptors."""
+    e0s = _binade(max(d[0] for d in descs))
+    ents = []
+    for k in range(2 * JB):
+        e, par, Q, L, ok, qs = e0s + k // 2, k & 1, 0.0, 0.0, True, []
+        for mx, e0t, q in descs:
+            kt = e - e0t
+            qv = q[2 * min(max(kt, 0), JB - 1) + par]
+            ok = ok and 0 <= kt < JB and qv == qv
+            Q += qv if ok else 0.0
+            ok = ok and Q < math.ldexp(1.0, e)
+            if ok:
+                par ^= int(math.ldexp(qv, 52 - e)) & 1
+            L = max(L, _next_up(mx + Q))
+            qs.append(Q)
+        ents.append((L if ok else NAN, qs))
+    return e0s, ents
+
+
+def _super_jump(rec, att):
+    """The fix walker's super jump: the tiles' entry states and the exit state, or None."""
+    e0s, ents = rec
+    if not att > 0.0:
+        return None
+    ab = _bits(att)
+    kb = (ab >> 52) - 1023 - e0s
+    if kb < 0 or kb >= JB:
+        return None
+    L, qs = ents[2 * kb + (ab & 1)]
+    x = att - qs[-1]
+    xb = _bits(x)
+    if not att > L or (xb >> 52) != (ab >> 52) or (xb & MANT) == 0:
+        return None
+    return [att] + [att - q for q in qs[:-1]], x
+
+
+@pytest.mark.timeout(300)
+def test_super_tile_jumps_are_exact():
+    """Records composed from SJ_TPS consecutive active tiles' descriptors: a super
+    jump lands on the state the step-by-step loop reaches, and every tile's entry
+    state it writes equals the loop's."""
+    jumps = checked = 0
+    for M, A, R in _band_M():
+        Ma = [float(v) for v in M if v != 0.0]  # the solve's compact (active) frames
+        traj = [0.0]
+        for m in Ma:
+            traj.append(_step(traj[-1], m, A, R))
+        span = SEG * SJ_TPS
+        for s0 in range(0, len(Ma) - span + 1, span):
+            segs = [Ma[s0 + t * SEG:s0 + (t + 1) * SEG] for t in range(SJ_TPS)]
+            rec = _compose_super([_describe(sg, R) for sg in segs])
+            true = traj[s0]
+            for att in (true, math.nextafter(true, math.inf), math.nextafter(true, -math.inf), true * 1.5,
+                        max(max(sg) for sg in segs) * 1.7):
+                checked += 1
+                r = _super_jump(rec, att)
+                if r is None:
+                    continue
+                jumps += 1
+                entries, x = r
+                y = att
+                for t, sg in enumerate(segs):
+                    assert entries[t] == y, (s0, t, att)
+                    for m in sg:
+                        y = _step(y, m, A, R)
+                assert x == y, (s0, att, x, y)
+    assert jumps > 0.2 * checked, (jumps, checked)
