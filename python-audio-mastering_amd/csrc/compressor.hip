@@ -596,11 +596,12 @@ __global__ void __launch_bounds__(64 * DESC_MAX_TPS) comp_describe_kernel(CompAr
     const bool live = valid && a.cnt[b][g] != 0;
     // tile order within the block: tile jt = (column block base) + l * TPS + kc
     flag[l * TPS + kc] = live ? 1 : 0;
-    if (threadIdx.x == 0) {  // active tiles of the chunk's earlier column blocks (comp_rms counts)
+    if (threadIdx.x < 64) {  // active tiles of the chunk's earlier column blocks (comp_rms counts), wave 0
         int32_t acc = 0;
         const int32_t *ct = a.cbtot[b] + cc * (a.SPC >> 6);
-        for (int64_t q = 0; q < cbl; ++q) acc += ct[q];
-        base_s = acc;
+        for (int64_t q = threadIdx.x; q < cbl; q += 64) acc += ct[q];
+        for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+        if (threadIdx.x == 0) base_s = acc;
     }
     __syncthreads();
     // exclusive scan of the flags in tile order: thread t takes entry t
@@ -869,7 +870,7 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
     const double *srec = a.sdesc[b];
     const int32_t *se0 = a.se0[b];
     const int64_t slast = (s / a.SPC) * a.SPC + a.SPC - 1;  // (clamp for the prefetches: the chunk's columns)
-    int e0_c = SJ_NONE, e0_n = SJ_NONE;   // se0 of cur, cur + 1
+    int e0_c = SJ_NONE, e0_n = SJ_NONE, e0_nn = SJ_NONE;  // se0 of cur, cur + 1, cur + 2
     int kb_c = -1, kb_n = -1;             // binade offsets the prefetched entries are for
     double old_c = 0.0, old_n = 0.0;      // stored entry states of cur's, cur + 1's first tile
     double ec[2][SJ_ENT], en[2][SJ_ENT];  // entries (parity 0, 1) of cur, cur + 1
@@ -883,6 +884,7 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
     if (sj) {
         e0_c = se0[cur];
         e0_n = se0[min(cur + 1, slast)];
+        e0_nn = se0[min(cur + 2, slast)];
         old_c = tst[st.ci0];
         kb_c = binade(att) - e0_c;
         ld_ent(cur, kb_c, ec);
@@ -895,7 +897,8 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
         for (int q = 0; q < 2; ++q)
 #pragma unroll
             for (int j = 0; j < SJ_ENT; ++j) ec[q][j] = en[q][j];
-        e0_n = se0[min(cur + 1, slast)];
+        e0_n = e0_nn;
+        e0_nn = se0[min(cur + 2, slast)];  // (used one super-tile later: its latency hides)
         old_c = old_n;
     };
     auto sj_prefetch = [&]() __attribute__((always_inline)) {  // cur + 1: first stored state, entries

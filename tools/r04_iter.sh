@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 if [ "$1" = "skip-tests" ]; then
   shift
 else
-  timeout -k 10 800 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_iter.log 2>&1
+  timeout -k 10 900 python -u -m pytest ${PYTEST_SEL:-tests} -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_iter.log 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/pytest_iter.log
   [ $rc -eq 0 ] || exit $rc
 fi
