@@ -61,6 +61,13 @@ __device__ __forceinline__ uint32_t rms_exact(double S, double n, float inv_n) {
     return n > 0.0 ? (uint32_t)r : 0u;
 }
 
+// correctly rounded m / d given rd = RN(1/d) (Markstein; tests/test_oracle.py)
+__device__ __forceinline__ double div_cr(double m, double d, double rd) {
+    const double q = m * rd;
+    const double rem = fma(-q, d, m);
+    return fma(rem, rd, q);
+}
+
 #ifndef MM_RMS_NB
 #define MM_RMS_NB 3
 #endif
@@ -144,7 +151,7 @@ __global__ void __launch_bounds__(256) comp_rms_kernel(CompArgs a) {
     float inv = n > 0.0 ? 1.0f / (float)n : 0.f;
     const uint32_t r0 = a.r0[b];
     const double *lut = a.lut[b];
-    const double rR = a.rcp_release[b];
+    const double Rf = a.release_frames[b], rR = a.rcp_release[b];
     constexpr uint32_t GS32 = 64;  // elements per row of a column block
     double *Mo = chunk_plane(a, b, cc);
     uint32_t e = col_elem(a, sc) + (uint32_t)(kc * a.TP) * GS32;  // row k*TP of column s
@@ -182,9 +189,9 @@ __global__ void __launch_bounds__(256) comp_rms_kernel(CompArgs a) {
     Pair buf[NB][B];
     double mq[B];
     int pn = 0;  // rows of the pending block (its gathers in flight)
-    // (max,+) release summary of the tile: any state E on entry leaves it at most at
-    // max(ce, E - De) when every attack is taken as an instant clamp (dec ~ M/R; a
-    // guess only, so not correctly rounded)
+    // (max,+) release summary of the tile for the pass-0 guesses: ce = the per-frame
+    // walk E <- max(M, E - M/R) from E = 0 (every attack an instant clamp; M/R
+    // correctly rounded, so ce is bit-exact: e_fold_tile), De ~ the tile's release
     double ce = 0.0, De = 0.0;
     // store the pending block: whole (every block but a partial last one) or its pn rows
     auto flush = [&](bool whole) __attribute__((always_inline)) {
@@ -194,7 +201,7 @@ __global__ void __launch_bounds__(256) comp_rms_kernel(CompArgs a) {
 #ifndef MM_RMS_NOSTORE  // (timing experiment only: no M plane)
                 Mo[e + (uint32_t)j * GS32] = mq[j];
 #endif
-                const double d = mq[j] * rR;
+                const double d = div_cr(mq[j], Rf, rR);
                 ce = fmax(mq[j], ce - d);
                 De += d;
             }
@@ -270,12 +277,6 @@ __global__ void __launch_bounds__(256) comp_rms_kernel(CompArgs a) {
     }
 }
 
-// correctly rounded m / d given rd = RN(1/d) (Markstein; tests/test_oracle.py)
-__device__ __forceinline__ double div_cr(double m, double d, double rd) {
-    const double q = m * rd;
-    const double rem = fma(-q, d, m);
-    return fma(rem, rd, q);
-}
 
 struct BandStep {
     double A, R, rA, rR;
@@ -658,52 +659,78 @@ __device__ __forceinline__ double next_up(double x) {
     return x > 0.0 ? __longlong_as_double(__double_as_longlong(x) + 1) : x;
 }
 
-// pass 0, lane = a full super-tile s with its first tile at compact index ci0
+// pass 0, lane = a full super-tile s with its first tile at compact index ci0 (the
+// tiles' records are loaded before any store: the stores could alias them)
 __device__ void compose_super(const CompArgs &a, int b, int64_t s, int64_t ci0) {
-    double mxs = 0.0;
+    double mxt[SJ_TPS], q[SJ_TPS][2 * JB];
 #pragma unroll
-    for (int t = 0; t < SJ_TPS; ++t) mxs = fmax(mxs, a.mmaxc[b][ci0 + t]);
-    const int e0s = binade(mxs);
-    double Q[2 * JB], L[2 * JB];
-    int par[2 * JB];
-    bool ok[2 * JB];
-#pragma unroll
-    for (int k = 0; k < 2 * JB; ++k) {
-        Q[k] = 0.0;
-        L[k] = 0.0;
-        par[k] = k & 1;
-        ok[k] = true;
-    }
-    double *rec = a.sdesc[b] + s * SREC;
     for (int t = 0; t < SJ_TPS; ++t) {
-        const double mx = a.mmaxc[b][ci0 + t];
-        const int e0t = binade(mx);
-        double q[2 * JB];
+        mxt[t] = a.mmaxc[b][ci0 + t];
         const double2 *r = reinterpret_cast<const double2 *>(a.descc[b] + (ci0 + t) * DREC);
 #pragma unroll
         for (int k = 0; k < JB; ++k) {
             const double2 v = r[k];
-            q[2 * k] = v.x;
-            q[2 * k + 1] = v.y;
-        }
-#pragma unroll
-        for (int k = 0; k < 2 * JB; ++k) {
-            const int e = e0s + k / 2, kt = e - e0t;
-            const int idx = 2 * min(max(kt, 0), JB - 1) + par[k];
-            double qv = q[0];
-#pragma unroll
-            for (int j = 1; j < 2 * JB; ++j) qv = idx == j ? q[j] : qv;
-            ok[k] = ok[k] && kt >= 0 && kt < JB && qv == qv;
-            Q[k] += ok[k] ? qv : 0.0;
-            ok[k] = ok[k] && Q[k] < ldexp(1.0, e);
-            if (ok[k]) par[k] ^= (int)((int64_t)ldexp(qv, 52 - e) & 1);  // qv / u, an exact integer
-            L[k] = fmax(L[k], next_up(mx + Q[k]));
-            rec[k * SJ_ENT + 1 + t] = Q[k];
+            q[t][2 * k] = v.x;
+            q[t][2 * k + 1] = v.y;
         }
     }
+    double mxs = 0.0;
 #pragma unroll
-    for (int k = 0; k < 2 * JB; ++k) rec[k * SJ_ENT] = ok[k] ? L[k] : __longlong_as_double(0x7ff8000000000000ll);
+    for (int t = 0; t < SJ_TPS; ++t) mxs = fmax(mxs, mxt[t]);
+    const int e0s = binade(mxs);
+    double rec[SREC];
+#pragma unroll
+    for (int k = 0; k < 2 * JB; ++k) {
+        double Q = 0.0, L = 0.0;
+        int par = k & 1;
+        bool ok = true;
+        const int e = e0s + k / 2;
+#pragma unroll
+        for (int t = 0; t < SJ_TPS; ++t) {
+            const int kt = e - binade(mxt[t]);
+            const int idx = 2 * min(max(kt, 0), JB - 1) + par;
+            double qv = q[t][0];
+#pragma unroll
+            for (int j = 1; j < 2 * JB; ++j) qv = idx == j ? q[t][j] : qv;
+            ok = ok && kt >= 0 && kt < JB && qv == qv;
+            Q += ok ? qv : 0.0;
+            ok = ok && Q < ldexp(1.0, e);
+            if (ok) par ^= (int)((int64_t)ldexp(qv, 52 - e) & 1);  // qv / u, an exact integer
+            L = fmax(L, next_up(mxt[t] + Q));
+            rec[k * SJ_ENT + 1 + t] = Q;
+        }
+        rec[k * SJ_ENT] = ok ? L : __longlong_as_double(0x7ff8000000000000ll);
+    }
+    double2 *out = reinterpret_cast<double2 *>(a.sdesc[b] + s * SREC);
+#pragma unroll
+    for (int k = 0; k < SREC / 2; ++k) out[k] = make_double2(rec[2 * k], rec[2 * k + 1]);
     a.se0[b][s] = e0s;
+}
+
+// The pass-0 guess across one tile: the exit of the per-frame (max,+) walk E <-
+// max(M, E - M/R) from entry E, bit for bit (tests/test_envelope_jumps.py) when the
+// tile's release-jump record covers E: E = 0 or below the tile's largest M clamps
+// in the tile and ends on ct (the walk from 0, comp_rms); above it the pure release
+// E - q (exact while it stays in E's binade: the offsets do not depend on M), max'ed
+// with ct (a walk that clamps ends on ct's values: the steps are monotone).  An
+// uncovered E takes E - Dt (a guess; exactness never depends on it).
+__device__ __forceinline__ double e_fold_tile(double E, double ct, double Dt, double mx, const double (&q)[2 * JB]) {
+    constexpr uint64_t MANT = (1ull << 52) - 1;
+    if (!(E > 0.0)) return ct;
+    const uint64_t ab = (uint64_t)__double_as_longlong(E);
+    const int k = (int)(ab >> 52) - 1023 - binade(mx);
+    if (k < 0) return ct;
+    double x = E - Dt;
+    if (k < JB) {
+        const int idx = 2 * k + (int)(ab & 1);
+        double qv = q[0];
+#pragma unroll
+        for (int j = 1; j < 2 * JB; ++j) qv = idx == j ? q[j] : qv;
+        const double y = E - qv;
+        const uint64_t yb = (uint64_t)__double_as_longlong(y);
+        if (y == y && (yb >> 52) == (ab >> 52) && (yb & MANT) != 0) x = y;
+    }
+    return fmax(ct, x);
 }
 
 // 3b. speculative pass.  grid: (ceil(GS/64), 3) of 64-lane blocks, lane =
@@ -713,7 +740,7 @@ __device__ void compose_super(const CompArgs &a, int b, int64_t s, int64_t ci0) 
 // active tiles before it (with `warmup` = 1, before a walk of the previous
 // super-tile).  Exactness never depends on the guess (the fix-up sweeps).
 constexpr int PASS0_BLOCK = 64, P0_MAXL = 64;  // lanes; tiles per walker (warm-up included)
-constexpr int E_TILES = 64;  // active tiles folded into a pass-0 guess (~8000 frames of release history)
+constexpr int E_TILES = 32;  // active tiles folded into a pass-0 guess (~4000 frames of release history)
 
 __global__ void __launch_bounds__(PASS0_BLOCK) comp_pass0_kernel(CompArgs a) {
     __shared__ uint32_t offs_lds[P0_MAXL][PASS0_BLOCK];
@@ -737,24 +764,35 @@ __global__ void __launch_bounds__(PASS0_BLOCK) comp_pass0_kernel(CompArgs a) {
     for (int i = 0; i < nmax; ++i)  // the walk's tile offsets (lanes past their own repeat their last)
         offs_lds[i][lane] = tile_off(a, ntot ? tl[cw0 + min(i, ntot - 1)] : 0);
     __syncthreads();
-    // the guess: the (max,+) envelope bound over the E_TILES active tiles before the
-    // walk (every attack an instant clamp, release at ~M/R per frame: the state
-    // after a loud stretch decays from its peak, where the M of the first frame
-    // left ~all super-tiles stale)
+    // the guess: the (max,+) walk of the E_TILES active tiles before the walk, from 0
+    // (every attack an instant clamp, release at M/R per frame): bit-exact across
+    // covered tiles, so after a loud stretch it carries the very release values a
+    // speculative walk that clamped at the same peak computes (the M of the first
+    // frame left ~all super-tiles stale)
     double att = 0.0;
     if (live && cw0 != cK) {
         const double2 *cd = reinterpret_cast<const double2 *>(a.cedc[b]);
-        int64_t i = max(cK, cw0 - E_TILES);
-        for (; i + 8 <= cw0; i += 8) {
-            double2 v[8];
+        const double *mxc = a.mmaxc[b];
+        const double2 *qd = reinterpret_cast<const double2 *>(a.descc[b]);
+        constexpr int EG = 4;  // tiles per load group
+        for (int64_t i = max(cK, cw0 - E_TILES); i < cw0; i += EG) {
+            double2 cdv[EG];
+            double mxv[EG], qv[EG][2 * JB];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) v[q] = cd[i + q];
+            for (int t = 0; t < EG; ++t) {
+                const int64_t it = min(i + t, cw0 - 1);
+                cdv[t] = cd[it];
+                mxv[t] = mxc[it];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) att = fmax(v[q].x, att - v[q].y);
-        }
-        for (; i < cw0; ++i) {
-            const double2 v = cd[i];
-            att = fmax(v.x, att - v.y);
+                for (int k = 0; k < JB; ++k) {
+                    const double2 v = qd[it * (DREC / 2) + k];
+                    qv[t][2 * k] = v.x;
+                    qv[t][2 * k + 1] = v.y;
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < EG; ++t)
+                if (i + t < cw0) att = e_fold_tile(att, cdv[t].x, cdv[t].y, mxv[t], qv[t]);
         }
     }
     if (a.sjump) {  // the super-tile's release-jump record (the sweeps' super jumps)

@@ -204,3 +204,59 @@ def test_super_tile_jumps_are_exact():
                         y = _step(y, m, A, R)
                 assert x == y, (s0, att, x, y)
     assert jumps > 0.2 * checked, (jumps, checked)
+
+
+def _e_walk(E, M, R):
+    """The (max,+) release envelope the pass-0 guesses follow: every attack an
+    instant clamp, E <- max(M, E - M/R) per frame (M/R correctly rounded)."""
+    for m in M:
+        E = max(m, E - m / R)
+    return E
+
+
+def _e_tile(E, ct, desc):
+    """compressor.hip e_fold_tile: the tile's E exit from its entry E, exactly as the
+    per-frame walk, from the tile's E walk from 0 (ct) and its release-jump record:
+    E - q when the pure release from E stays in its binade (the release offsets do not
+    depend on M), max'ed with ct (a trajectory that clamps ends on ct's: monotone
+    steps); None when no record covers E (the device then takes E - D: inexact)."""
+    if E == 0.0:
+        return ct
+    mx, e0, q = desc
+    eb = _binade(E)
+    if eb < e0:  # below the tile's largest M: it clamps there
+        return ct
+    if eb - e0 >= JB:
+        return None
+    x = E - q[2 * (eb - e0) + (_bits(E) & 1)]
+    if math.isnan(x):
+        return None
+    xb = _bits(x)
+    if (xb >> 52) != (_bits(E) >> 52) or (xb & MANT) == 0:
+        return None
+    return max(ct, x)
+
+
+@pytest.mark.timeout(300)
+def test_e_fold_by_tiles_is_exact():
+    """The pass-0 guess folded tile by tile equals the per-frame (max,+) walk bit for
+    bit whenever the tile records cover the state (so a guess coincides with a
+    speculative walk's release values, as tools/study/envelope_model.c assumes)."""
+    total = covered = 0
+    for M, A, R in _band_M():
+        Ma = [float(v) for v in M if v != 0.0]
+        segs = [Ma[s0:s0 + SEG] for s0 in range(0, len(Ma) - SEG + 1, SEG)]
+        E_frame = E_tile = 0.0
+        for sg in segs:
+            ct = _e_walk(0.0, sg, R)
+            nxt = _e_tile(E_tile, ct, _describe(sg, R))
+            E_frame = _e_walk(E_frame, sg, R)
+            total += 1
+            if nxt is None:  # not covered: restart the comparison from the exact value
+                E_tile = E_frame
+                continue
+            covered += 1
+            assert nxt == E_frame
+            E_tile = nxt
+    print(f"e fold: {covered} of {total} tiles covered by their records")
+    assert covered > 0.9 * total

@@ -40,5 +40,8 @@ for w in C2 C2hot; do
     || { tail -5 gpurun_out/ft_$w.err; exit 1; }
   echo "fix trace $w"; python tools/fix_fit.py gpurun_out/fixdump_$w.bin
 done
+for lib in $(ls build/var/*.so 2>/dev/null); do
+  run C2_$(basename $lib .so) "MM_LIB=$PWD/$lib" --workload C2 || exit 1
+done
 run C3 - --workload C3 || exit 1
 run C5 - --workload C5 || exit 1
