@@ -72,6 +72,7 @@ __device__ __forceinline__ double div_cr(double m, double d, double rd) {
 #define MM_RMS_NB 3
 #endif
 constexpr int RMS_B = 8;  // frames per load block of comp_rms
+constexpr int RANK_GROUP = 256;  // tiles per comp_describe block (a chunk's rank groups: GPC = ceil(K / 256))
 
 // Super-tile-major M plane of a band: frame n of tile g — the k-th tile of
 // super-tile s — is row k*TP + n of column s (TP = T rounded up to whole walk load
@@ -98,14 +99,13 @@ __device__ __forceinline__ double *chunk_plane(const CompArgs &a, int b, int64_t
     return a.Ms[b] + c * a.chunk_elems;
 }
 
-// 1. rms and M per frame.  grid: (GS * TPS / 256, 3 bands) of 256-thread blocks,
-// one wave per (column block, position k): wave v handles tile k = v % TPS of the 64
-// super-tiles (columns) of column block v / TPS, lane l the one of column 64 (v /
-// TPS) + l.  SPC is a multiple of 64, so a column block lies in one chunk and the
-// wave's 64 lanes store row k*T + n of 64 consecutive columns: every M store is
-// one 512-byte run (round 3 mapped lanes to consecutive tiles: 8 runs of 64 B per
-// store).  The band loads are TPS tiles apart across the lanes (the block's TPS
-// waves share those lines).  The window [max(chunk0, f-look), f) slides one frame
+// 1. rms and M per frame.  grid: (chunks * WPC / 4, 3 bands) of 256-thread blocks,
+// WPC = ceil(K / 64) waves per chunk: wave m of chunk c takes its tiles 64 m ..
+// 64 m + 63 (lane = tile), so the band loads are coalesced and, the chunk's columns
+// starting on a 64-column block (SPC is a multiple of 64), the wave's tiles are 64 /
+// TPS whole columns aligned to them: every M store is TPS aligned runs of 512 / TPS
+// bytes (4 whole cache lines at TPS = 4; round 3's globally aligned waves stored 8
+// misaligned runs of 64 B).  The window [max(chunk0, f-look), f) slides one frame
 // per step: + frame f-1 (this lane's own previous frame), - frame f-1-look (up to
 // ~4 tiles back: another tile's data).  The window sum is an exact integer held in
 // a double.  M = lut[r] is gathered ONCE here (a block of RMS_B frames' gathers is
@@ -117,12 +117,13 @@ __device__ __forceinline__ double *chunk_plane(const CompArgs &a, int b, int64_t
 __global__ void __launch_bounds__(256) comp_rms_kernel(CompArgs a) {
     const int b = blockIdx.y;
     const int64_t wv = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int kc = (int)(wv % a.TPS);
-    const int64_t sc = (wv / a.TPS) * 64 + (threadIdx.x & 63);
-    const int64_t cc = sc / a.SPC;
-    const int64_t jt = (sc - cc * a.SPC) * a.TPS + kc;
+    const int64_t WPC = ((int64_t)a.K + 63) / 64;
+    const int64_t cc = wv / WPC;
+    const int64_t jt = (wv - cc * WPC) * 64 + (threadIdx.x & 63);
     const int64_t g = cc * a.K + jt;
-    if (jt >= a.K || g >= a.G) return;  // past the chunk's tiles (its last super-tile) or the track
+    if (jt >= a.K || g >= a.G) return;  // past the chunk's tiles (its last wave) or the track
+    const int64_t sc = cc * a.SPC + jt / a.TPS;
+    const int kc = (int)(jt % a.TPS);
     const short2 *x = a.band[b];
     const int look = a.look[b];
     const int T = a.T;
@@ -258,10 +259,10 @@ __global__ void __launch_bounds__(256) comp_rms_kernel(CompArgs a) {
     for (int i = max(len, 0); i < a.TP; ++i, e += GS32) Mo[e] = 0.0;
     a.cnt[b][g] = active;
     a.mmax[b][g] = lut[rmx];
-    {  // active tiles of the column block (comp_describe ranks the chunk's active tiles from them)
+    {  // active tiles of the rank group (comp_describe ranks the chunk's active tiles from them)
         const int na = (int)__popcll(__ballot(active != 0));
         if (__lane_id() == __builtin_amdgcn_readfirstlane(__lane_id()) && na)
-            atomicAdd(a.cbtot[b] + (sc >> 6), na);
+            atomicAdd(a.cbtot[b] + cc * a.GPC + jt / RANK_GROUP, na);
     }
     reinterpret_cast<double2 *>(a.ced[b])[g] = make_double2(ce, De);
     // per-chunk active count (statistics): one atomic per wave when all 64 lanes
@@ -563,61 +564,46 @@ struct Describer {
     }
 };
 
-// 2. links + describers, ONE launch.  grid: (column blocks, 3), a block of
-// 64 * TPS threads = one column block (64 super-tiles x TPS tiles = 64 TPS
-// consecutive tiles of one chunk), lanes mapped to tiles as in comp_rms (wave k:
-// tile position k of the 64 columns), so the describers' M loads are 512-byte runs.
+// 2. links + describers, ONE launch.  grid: (chunks * GPC, 3), a block of 256
+// threads = one rank group of 256 consecutive tiles of a chunk (lane = tile, waves
+// aligned to the chunk's columns as in comp_rms: the describers' M loads are whole
+// cache lines).
 //  * links: ranks the chunk's active tiles (rank[g] = active tiles before g in its
-//    chunk: the counts comp_rms left per column block for the blocks before this
-//    one, plus a scan over the block's tiles in tile order), lists them at compact
-//    index ci = chunk * K + rank (tl = the tile, mmaxc = its largest M, cedc = its
-//    (max,+) summary) and counts them (nact[c], by the chunk's last block);
+//    chunk: the counts comp_rms left per rank group for the groups before this one,
+//    plus a scan over the block's tiles), lists them at compact index ci = chunk * K
+//    + rank (tl = the tile, mmaxc = its largest M, cedc = its (max,+) summary) and
+//    counts them (nact[c], by the chunk's last group);
 //  * describers: an active tile's release-jump record (Describer).
 // (Round 3 ran the links as one 1024-thread block per chunk and band: 30 blocks
 // for a 5-min track, 26 us of latency before the describers' own launch.)
 #ifndef MM_DESC_NB
 #define MM_DESC_NB 1
 #endif
-constexpr int DESC_MAX_TPS = 16;  // block = 64 * TPS <= 1024 threads
 
-__global__ void __launch_bounds__(64 * DESC_MAX_TPS) comp_describe_kernel(CompArgs a) {
-    __shared__ int32_t wsum[DESC_MAX_TPS], base_s;
-    __shared__ uint8_t flag[64 * DESC_MAX_TPS];
-    __shared__ int32_t pre[64 * DESC_MAX_TPS];
+__global__ void __launch_bounds__(RANK_GROUP) comp_describe_kernel(CompArgs a) {
+    __shared__ int32_t wsum[RANK_GROUP / 64], base_s;
     const int b = blockIdx.y;
-    const int TPS = a.TPS, NT = 64 * TPS;
-    const int kc = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const int64_t cb = blockIdx.x;  // column block
-    const int64_t sc = cb * 64 + l;
-    const int64_t cc = sc / a.SPC;
-    const int64_t cbl = (sc - cc * a.SPC) >> 6;  // column block within the chunk
-    const int64_t jt = (sc - cc * a.SPC) * TPS + kc;
+    const int t = threadIdx.x;
+    const int64_t cc = blockIdx.x / a.GPC, q = blockIdx.x - cc * a.GPC;  // chunk, group
+    const int64_t jt = q * RANK_GROUP + t;
     const int64_t g = cc * a.K + jt;
     const bool valid = jt < a.K && g < a.G;
     const bool live = valid && a.cnt[b][g] != 0;
-    // tile order within the block: tile jt = (column block base) + l * TPS + kc
-    flag[l * TPS + kc] = live ? 1 : 0;
-    if (threadIdx.x < 64) {  // active tiles of the chunk's earlier column blocks (comp_rms counts), wave 0
+    if (t < 64) {  // active tiles of the chunk's earlier groups (comp_rms counts), wave 0
         int32_t acc = 0;
-        const int32_t *ct = a.cbtot[b] + cc * (a.SPC >> 6);
-        for (int64_t q = threadIdx.x; q < cbl; q += 64) acc += ct[q];
+        const int32_t *ct = a.cbtot[b] + cc * a.GPC;
+        for (int64_t i = t; i < q; i += 64) acc += ct[i];
         for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-        if (threadIdx.x == 0) base_s = acc;
+        if (t == 0) base_s = acc;
     }
-    __syncthreads();
-    // exclusive scan of the flags in tile order: thread t takes entry t
-    const int t = threadIdx.x;
-    const bool f = flag[t] != 0;
-    const uint64_t bal = __ballot(f);
+    // exclusive scan of the live flags in tile order
+    const uint64_t bal = __ballot(live);
     const int wp = (int)__popcll(bal & ((1ull << (t & 63)) - 1ull));
     if ((t & 63) == 0) wsum[t >> 6] = (int32_t)__popcll(bal);
     __syncthreads();
-    int32_t woff = base_s;
-    for (int w = 0; w < (t >> 6); ++w) woff += wsum[w];
-    pre[t] = woff + wp;
-    if (t == NT - 1 && cbl == (a.SPC >> 6) - 1) a.nact[b][cc] = woff + wp + (f ? 1 : 0);  // the chunk's last block
-    __syncthreads();
-    const int32_t r = pre[l * TPS + kc];
+    int32_t r = base_s + wp;
+    for (int w = 0; w < (t >> 6); ++w) r += wsum[w];
+    if (t == RANK_GROUP - 1 && q == a.GPC - 1) a.nact[b][cc] = r + (live ? 1 : 0);  // the chunk's last group
     const int64_t ci = cc * a.K + r;
     if (valid) a.rank[b][g] = r;
     if (live) {
@@ -740,7 +726,7 @@ __device__ __forceinline__ double e_fold_tile(double E, double ct, double Dt, do
 // active tiles before it (with `warmup` = 1, before a walk of the previous
 // super-tile).  Exactness never depends on the guess (the fix-up sweeps).
 constexpr int PASS0_BLOCK = 64, P0_MAXL = 64;  // lanes; tiles per walker (warm-up included)
-constexpr int E_TILES = 32;  // active tiles folded into a pass-0 guess (~4000 frames of release history)
+constexpr int E_TILES = 32;  // active tiles folded into a pass-0 guess by default (~4000 frames of release history)
 
 __global__ void __launch_bounds__(PASS0_BLOCK) comp_pass0_kernel(CompArgs a) {
     __shared__ uint32_t offs_lds[P0_MAXL][PASS0_BLOCK];
@@ -775,7 +761,7 @@ __global__ void __launch_bounds__(PASS0_BLOCK) comp_pass0_kernel(CompArgs a) {
         const double *mxc = a.mmaxc[b];
         const double2 *qd = reinterpret_cast<const double2 *>(a.descc[b]);
         constexpr int EG = 4;  // tiles per load group
-        for (int64_t i = max(cK, cw0 - E_TILES); i < cw0; i += EG) {
+        for (int64_t i = max(cK, cw0 - a.e_tiles); i < cw0; i += EG) {
             double2 cdv[EG];
             double mxv[EG], qv[EG][2 * JB];
 #pragma unroll
@@ -960,8 +946,14 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
         if (++ci < ce) return true;
         st_sc1(end + cur, att);
         if (st.last) return false;  // the chunk's last super-tile
+        // the Jacobi sweep stops here (its walkers are every stale super-tile: a chain
+        // through a successor would run behind it; the successor is stale next sweep,
+        // which this walk's own `changed` flag queues); run-head sweeps continue if the
+        // successor could be claimed (else its owner read an older end of cur: stale
+        // next sweep)
+        if (!a.heads && !a.jacobi_continue) return false;
         if (!a.heads) nx_claimed = comp_claim(a, b, cur + 1);
-        if (!nx_claimed) return false;  // its owner read an older end of cur: it is stale (flagged) next sweep
+        if (!nx_claimed) return false;
         ++cur;
         st = super_of(a, b, cur);
         a.start[b][cur] = att;
@@ -1102,9 +1094,14 @@ __global__ void __launch_bounds__(192, MM_APPLY_MINB) comp_apply_kernel(CompArgs
     const int b = threadIdx.x / APPLY_TILES;
     const int lane = threadIdx.x % APPLY_TILES;
     const int64_t G = a.G;
-    const int64_t g0 = (int64_t)blockIdx.x * APPLY_TILES;
+    // chunk-aligned blocks (the M rows of a block's 64 tiles are whole cache lines)
+    const int64_t WPC = ((int64_t)a.K + APPLY_TILES - 1) / APPLY_TILES;
+    const int64_t cb = blockIdx.x / WPC;
+    const int64_t j0 = (blockIdx.x - cb * WPC) * APPLY_TILES;  // first tile of the block in its chunk
+    const int64_t g0 = cb * a.K + j0;
     const int64_t g = g0 + lane;
-    const bool valid = g < G;
+    const int jn = (int)min((int64_t)APPLY_TILES, a.K - j0);  // the block's tiles (the chunk's last block: fewer)
+    const bool valid = lane < jn && g < G;
     const int T = a.T;
     const int len = valid ? (int)min((int64_t)T, a.N_proc - g * T) : 0;
     const BandStep bs = band_step(a, b);
@@ -1201,7 +1198,7 @@ __global__ void __launch_bounds__(192, MM_APPLY_MINB) comp_apply_kernel(CompArgs
             const int j = p / APPLY_TILES, tl = p % APPLY_TILES;
             const int64_t gt = g0 + tl;
             const int n = n0 + j;
-            if (gt < G && n < (int)min((int64_t)T, a.N_proc - gt * T)) {
+            if (tl < jn && gt < G && n < (int)min((int64_t)T, a.N_proc - gt * T)) {
                 const short2 lo = lds[0][j][tl], mi = lds[1][j][tl], hi = lds[2][j][tl];
                 const int16_t l = sat16(sat16((int32_t)lo.x + mi.x) + hi.x);
                 const int16_t rr = sat16(sat16((int32_t)lo.y + mi.y) + hi.y);

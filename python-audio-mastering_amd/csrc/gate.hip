@@ -37,36 +37,51 @@ __device__ __forceinline__ double gate_block_z(const GateArgs &a, int64_t j) {
     return a.scale * acc;
 }
 
-// sum and count over the block (tree order), result broadcast to every thread
+// sum and count over the block, result broadcast to every thread: a fixed-order
+// butterfly within each wave, then the waves' partials in order (deterministic)
 __device__ __forceinline__ void gate_reduce(double &sum, long long &cnt, double *rs, long long *rc) {
     const int t = threadIdx.x;
-    rs[t] = sum;
-    rc[t] = cnt;
-    __syncthreads();
-    for (int d = GATE_THREADS / 2; d > 0; d >>= 1) {
-        if (t < d) {
-            rs[t] += rs[t + d];
-            rc[t] += rc[t + d];
-        }
-        __syncthreads();
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        sum += __shfl_xor(sum, o);
+        cnt += __shfl_xor(cnt, o);
     }
-    sum = rs[0];
-    cnt = rc[0];
+    if ((t & 63) == 0) {
+        rs[t >> 6] = sum;
+        rc[t >> 6] = cnt;
+    }
+    __syncthreads();
+    sum = 0.0;
+    cnt = 0;
+#pragma unroll
+    for (int w = 0; w < GATE_THREADS / 64; ++w) {
+        sum += rs[w];
+        cnt += rc[w];
+    }
     __syncthreads();
 }
 
+constexpr int GATE_CACHE = 4;  // block energies a thread keeps between the two gates
+
 __global__ void __launch_bounds__(GATE_THREADS) gate_kernel(GateArgs a) {
-    __shared__ double rs[GATE_THREADS];
-    __shared__ long long rc[GATE_THREADS];
+    __shared__ double rs[GATE_THREADS / 64];
+    __shared__ long long rc[GATE_THREADS / 64];
     const int t = threadIdx.x;
     const int64_t j0 = a.trk_blk ? a.trk_blk[blockIdx.x] : 0;
     const int64_t j1 = a.trk_blk ? a.trk_blk[blockIdx.x + 1] : a.n_blocks;
     double *out = a.out + 2 * blockIdx.x;
+    double zc[GATE_CACHE], lc[GATE_CACHE];  // the thread's first blocks (a 5-min track: 3 each)
     double sum = 0.0;
     long long cnt = 0;
-    for (int64_t j = j0 + t; j < j1; j += GATE_THREADS) {
+    int i = 0;
+    for (int64_t j = j0 + t; j < j1; j += GATE_THREADS, ++i) {
         const double z = gate_block_z(a, j);
-        if (-0.691 + 10.0 * log10(z) >= -70.0) {
+        const double l = -0.691 + 10.0 * log10(z);
+        if (i < GATE_CACHE) {
+            zc[i] = z;
+            lc[i] = l;
+        }
+        if (l >= -70.0) {
             sum += z;
             ++cnt;
         }
@@ -76,9 +91,16 @@ __global__ void __launch_bounds__(GATE_THREADS) gate_kernel(GateArgs a) {
     const double gamma_r = -0.691 + 10.0 * log10(mean_abs) - 10.0;
     sum = 0.0;
     cnt = 0;
-    for (int64_t j = j0 + t; j < j1; j += GATE_THREADS) {
-        const double z = gate_block_z(a, j);
-        const double l = -0.691 + 10.0 * log10(z);
+    i = 0;
+    for (int64_t j = j0 + t; j < j1; j += GATE_THREADS, ++i) {
+        double z, l;
+        if (i < GATE_CACHE) {
+            z = zc[i];
+            l = lc[i];
+        } else {
+            z = gate_block_z(a, j);
+            l = -0.691 + 10.0 * log10(z);
+        }
         if (l > gamma_r && l > -70.0) {
             sum += z;
             ++cnt;

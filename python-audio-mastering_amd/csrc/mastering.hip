@@ -328,8 +328,9 @@ static int comp_sweeps(mm_ctx *c, int n) {
 // gains + overlay into q2, every tile starting from its stored entry state
 static int comp_back(mm_ctx *c) {
     const CompArgs &ca = c->ca;
-    return launch(c, "comp_apply", comp_apply_kernel, dim3(blocks_for(ca.G, APPLY_TILES)), dim3(3 * APPLY_TILES), 0,
-                  ca);
+    const int64_t nchunks = ca.GS / ca.SPC;  // (chunk-aligned blocks of APPLY_TILES tiles)
+    return launch(c, "comp_apply", comp_apply_kernel,
+                  dim3((unsigned)(nchunks * ((ca.K + APPLY_TILES - 1) / APPLY_TILES))), dim3(3 * APPLY_TILES), 0, ca);
 }
 
 // Pinned readback block of one chain pass (offsets in bytes): look-back error
@@ -432,7 +433,7 @@ static int solve_geometry(const mm_job *j, mm_solve_geom *g) {
     if (K < 1 || T < 1 || j->frames_proc < 0) return MM_ERR_ARG;
     const int64_t G = (j->frames_proc + T - 1) / T;
     *g = mm_solve_geom{};
-    g->tps = std::max(1, std::min((j->comp_super + T / 2) / T, DESC_MAX_TPS));  // (comp_describe: 64 TPS threads)
+    g->tps = std::max(1, std::min((j->comp_super + T / 2) / T, P0_MAXL / 2));  // (a walk plus a warm-up super-tile)
     g->chunks = (G + K - 1) / K;
     g->cols_per_chunk = (((int64_t)K + g->tps - 1) / g->tps + 63) / 64 * 64;
     g->tile_rows = (T + WB - 1) / WB * WB;
@@ -489,6 +490,7 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     const int64_t nchunks = sg.chunks;
     ca.TPS = sg.tps;
     ca.SPC = sg.cols_per_chunk;
+    ca.GPC = ((int64_t)K + RANK_GROUP - 1) / RANK_GROUP;
     ca.GS = nchunks * ca.SPC;
     const int64_t NS = ca.GS;
     short2 *q2;
@@ -514,6 +516,9 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     RET(get_buf(c, "comp_nact", (size_t)3 * nchunks, &nacts));
     ca.jumps = getenv("MM_COMP_NOJUMP") ? 0 : 1;  // diagnostics: results must not change
     ca.sjump = ca.jumps && !getenv("MM_COMP_NOSJUMP") && ca.TPS == SJ_TPS ? 1 : 0;
+    ca.jacobi_continue = getenv("MM_JACOBI_CONTINUE") ? 1 : 0;  // (tuning experiments)
+    ca.e_tiles = E_TILES;
+    if (const char *e = getenv("MM_E_TILES")) ca.e_tiles = std::max(0, atoi(e));  // (tuning experiments)
     double *sdesc;
     int32_t *se0s;
     RET(get_buf(c, "comp_sdesc", ca.sjump ? (size_t)3 * NS * SREC : 1, &sdesc));
@@ -573,10 +578,12 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
         ca.claim[b] = claims + (size_t)b * NS;
         ca.sdesc[b] = ca.sjump ? sdesc + (size_t)b * NS * SREC : nullptr;
         ca.se0[b] = ca.sjump ? se0s + (size_t)b * NS : nullptr;
-        ca.cbtot[b] = reinterpret_cast<int32_t *>(claims + (size_t)3 * NS) + (size_t)b * (NS / 64);
+        ca.cbtot[b] = reinterpret_cast<int32_t *>(claims + (size_t)3 * NS) + (size_t)b * nchunks * ca.GPC;
     }
-    RET(launch(c, "comp_rms", comp_rms_kernel, dim3(blocks_for(NS / 64 * ca.TPS, 4), 3), dim3(256), 0, ca));
-    RET(launch(c, "comp_describe", comp_describe_kernel, dim3((unsigned)(NS / 64), 3), dim3(64 * ca.TPS), 0, ca));
+    const int64_t WPC = ((int64_t)K + 63) / 64;  // comp_rms / comp_apply waves (blocks) per chunk
+    RET(launch(c, "comp_rms", comp_rms_kernel, dim3(blocks_for(nchunks * WPC, 4), 3), dim3(256), 0, ca));
+    RET(launch(c, "comp_describe", comp_describe_kernel, dim3((unsigned)(nchunks * ca.GPC), 3), dim3(RANK_GROUP), 0,
+               ca));
     RET(launch(c, "comp_pass0", comp_pass0_kernel, dim3(blocks_for(NS, PASS0_BLOCK), 3), dim3(PASS0_BLOCK), 0, ca));
     c->comp_on = true;
     c->ca = ca;
@@ -614,7 +621,7 @@ static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
         nch = sg.chunks;
         spc = sg.cols_per_chunk;
     }
-    RET(setup_control(c, nblk, nch, 3 * nch * spc + 3 * nch * spc / 64));  // claim stamps, column-block counts
+    RET(setup_control(c, nblk, nch, 3 * nch * spc + 3 * nch * ((K + RANK_GROUP - 1) / RANK_GROUP)));  // claim stamps, group counts
 
     EqArgs ea{};
     ea.in = j->in_kind == MM_IN_I16 ? nullptr : static_cast<const float *>(d_in);
