@@ -152,8 +152,7 @@ struct CompArgs {
     double *mmax[3];           // per tile: largest M
     double *ced[3];            // per tile: (max,+) release summary {c, D} (double2; comp_rms)
     int32_t *total[3];         // per chunk: active frames (statistics)
-    int32_t *cbtot[3];         // per rank group (256 tiles of a chunk): active tiles (comp_rms; zeroed per chain)
-    int64_t GPC;               // rank groups per chunk: ceil(K / 256)
+    int32_t *cbtot[3];         // per column block: active tiles (comp_rms; zeroed per chain)
     int32_t *rank[3];          // per tile: active tiles before it in its chunk (comp_describe)
     int32_t *nact[3];          // per chunk: active tiles
     // per active tile at compact index ci = chunk * K + rank:
@@ -171,7 +170,7 @@ struct CompArgs {
     int32_t *se0[3];           // per super-tile: binade of its largest M (SJ_NONE: no record)
     uint32_t stamp;            // this sweep's stamp (> every earlier one of the chain)
     int heads;                 // 0: Jacobi sweep (every stale super-tile walks); 1: run heads only
-    int jacobi_continue;       // a Jacobi walker continues into a successor it can claim (MM_JACOBI_CONTINUE=1)
+    int jacobi_stop;           // a Jacobi walker stops at its super-tile's end (MM_JACOBI_STOP=1: experiments)
     int e_tiles;               // active tiles of a pass-0 guess's (max,+) fold (MM_E_TILES; E_TILES)
     unsigned int *changed;
     unsigned long long *walked;  // [0] frames re-walked, [1] frames jumped by the fix-up sweeps (statistics)

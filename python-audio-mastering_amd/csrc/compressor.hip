@@ -72,7 +72,6 @@ __device__ __forceinline__ double div_cr(double m, double d, double rd) {
 #define MM_RMS_NB 3
 #endif
 constexpr int RMS_B = 8;  // frames per load block of comp_rms
-constexpr int RANK_GROUP = 256;  // tiles per comp_describe block (a chunk's rank groups: GPC = ceil(K / 256))
 
 // Super-tile-major M plane of a band: frame n of tile g — the k-th tile of
 // super-tile s — is row k*TP + n of column s (TP = T rounded up to whole walk load
@@ -99,13 +98,14 @@ __device__ __forceinline__ double *chunk_plane(const CompArgs &a, int b, int64_t
     return a.Ms[b] + c * a.chunk_elems;
 }
 
-// 1. rms and M per frame.  grid: (chunks * WPC / 4, 3 bands) of 256-thread blocks,
-// WPC = ceil(K / 64) waves per chunk: wave m of chunk c takes its tiles 64 m ..
-// 64 m + 63 (lane = tile), so the band loads are coalesced and, the chunk's columns
-// starting on a 64-column block (SPC is a multiple of 64), the wave's tiles are 64 /
-// TPS whole columns aligned to them: every M store is TPS aligned runs of 512 / TPS
-// bytes (4 whole cache lines at TPS = 4; round 3's globally aligned waves stored 8
-// misaligned runs of 64 B).  The window [max(chunk0, f-look), f) slides one frame
+// 1. rms and M per frame.  grid: (GS * TPS / 256, 3 bands) of 256-thread blocks,
+// one wave per (column block, position k): wave v handles tile k = v % TPS of the 64
+// super-tiles (columns) of column block v / TPS, lane l the one of column 64 (v /
+// TPS) + l.  SPC is a multiple of 64, so a column block lies in one chunk and the
+// wave's 64 lanes store row k*T + n of 64 consecutive columns: every M store is
+// one 512-byte run (round 3 mapped lanes to consecutive tiles: 8 runs of 64 B per
+// store).  The band loads are TPS tiles apart across the lanes (the block's TPS
+// waves share those lines).  The window [max(chunk0, f-look), f) slides one frame
 // per step: + frame f-1 (this lane's own previous frame), - frame f-1-look (up to
 // ~4 tiles back: another tile's data).  The window sum is an exact integer held in
 // a double.  M = lut[r] is gathered ONCE here (a block of RMS_B frames' gathers is
@@ -117,13 +117,12 @@ __device__ __forceinline__ double *chunk_plane(const CompArgs &a, int b, int64_t
 __global__ void __launch_bounds__(256) comp_rms_kernel(CompArgs a) {
     const int b = blockIdx.y;
     const int64_t wv = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int64_t WPC = ((int64_t)a.K + 63) / 64;
-    const int64_t cc = wv / WPC;
-    const int64_t jt = (wv - cc * WPC) * 64 + (threadIdx.x & 63);
+    const int kc = (int)(wv % a.TPS);
+    const int64_t sc = (wv / a.TPS) * 64 + (threadIdx.x & 63);
+    const int64_t cc = sc / a.SPC;
+    const int64_t jt = (sc - cc * a.SPC) * a.TPS + kc;
     const int64_t g = cc * a.K + jt;
-    if (jt >= a.K || g >= a.G) return;  // past the chunk's tiles (its last wave) or the track
-    const int64_t sc = cc * a.SPC + jt / a.TPS;
-    const int kc = (int)(jt % a.TPS);
+    if (jt >= a.K || g >= a.G) return;  // past the chunk's tiles (its last super-tile) or the track
     const short2 *x = a.band[b];
     const int look = a.look[b];
     const int T = a.T;
@@ -259,10 +258,10 @@ __global__ void __launch_bounds__(256) comp_rms_kernel(CompArgs a) {
     for (int i = max(len, 0); i < a.TP; ++i, e += GS32) Mo[e] = 0.0;
     a.cnt[b][g] = active;
     a.mmax[b][g] = lut[rmx];
-    {  // active tiles of the rank group (comp_describe ranks the chunk's active tiles from them)
+    {  // active tiles of the column block (comp_describe ranks the chunk's active tiles from them)
         const int na = (int)__popcll(__ballot(active != 0));
         if (__lane_id() == __builtin_amdgcn_readfirstlane(__lane_id()) && na)
-            atomicAdd(a.cbtot[b] + cc * a.GPC + jt / RANK_GROUP, na);
+            atomicAdd(a.cbtot[b] + (sc >> 6), na);
     }
     reinterpret_cast<double2 *>(a.ced[b])[g] = make_double2(ce, De);
     // per-chunk active count (statistics): one atomic per wave when all 64 lanes
@@ -364,6 +363,10 @@ __device__ __forceinline__ Super super_of(const CompArgs &a, int b, int64_t s) {
 #endif
 constexpr int WB = MM_WALK_B;   // rows per load block (divides TP)
 constexpr int WNB = MM_WALK_NB; // blocks in flight (sweep walkers)
+#ifndef MM_FIX_WNB
+#define MM_FIX_WNB MM_WALK_NB
+#endif
+constexpr int FIX_WNB = MM_FIX_WNB;  // blocks in flight of a fix-up walker's tile walk
 #ifndef MM_P0_NB
 #define MM_P0_NB 2
 #endif
@@ -564,46 +567,61 @@ struct Describer {
     }
 };
 
-// 2. links + describers, ONE launch.  grid: (chunks * GPC, 3), a block of 256
-// threads = one rank group of 256 consecutive tiles of a chunk (lane = tile, waves
-// aligned to the chunk's columns as in comp_rms: the describers' M loads are whole
-// cache lines).
+// 2. links + describers, ONE launch.  grid: (column blocks, 3), a block of
+// 64 * TPS threads = one column block (64 super-tiles x TPS tiles = 64 TPS
+// consecutive tiles of one chunk), lanes mapped to tiles as in comp_rms (wave k:
+// tile position k of the 64 columns), so the describers' M loads are 512-byte runs.
 //  * links: ranks the chunk's active tiles (rank[g] = active tiles before g in its
-//    chunk: the counts comp_rms left per rank group for the groups before this one,
-//    plus a scan over the block's tiles), lists them at compact index ci = chunk * K
-//    + rank (tl = the tile, mmaxc = its largest M, cedc = its (max,+) summary) and
-//    counts them (nact[c], by the chunk's last group);
+//    chunk: the counts comp_rms left per column block for the blocks before this
+//    one, plus a scan over the block's tiles in tile order), lists them at compact
+//    index ci = chunk * K + rank (tl = the tile, mmaxc = its largest M, cedc = its
+//    (max,+) summary) and counts them (nact[c], by the chunk's last block);
 //  * describers: an active tile's release-jump record (Describer).
 // (Round 3 ran the links as one 1024-thread block per chunk and band: 30 blocks
 // for a 5-min track, 26 us of latency before the describers' own launch.)
 #ifndef MM_DESC_NB
 #define MM_DESC_NB 1
 #endif
+constexpr int DESC_MAX_TPS = 16;  // block = 64 * TPS <= 1024 threads
 
-__global__ void __launch_bounds__(RANK_GROUP) comp_describe_kernel(CompArgs a) {
-    __shared__ int32_t wsum[RANK_GROUP / 64], base_s;
+__global__ void __launch_bounds__(64 * DESC_MAX_TPS) comp_describe_kernel(CompArgs a) {
+    __shared__ int32_t wsum[DESC_MAX_TPS], base_s;
+    __shared__ uint8_t flag[64 * DESC_MAX_TPS];
+    __shared__ int32_t pre[64 * DESC_MAX_TPS];
     const int b = blockIdx.y;
-    const int t = threadIdx.x;
-    const int64_t cc = blockIdx.x / a.GPC, q = blockIdx.x - cc * a.GPC;  // chunk, group
-    const int64_t jt = q * RANK_GROUP + t;
+    const int TPS = a.TPS, NT = 64 * TPS;
+    const int kc = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int64_t cb = blockIdx.x;  // column block
+    const int64_t sc = cb * 64 + l;
+    const int64_t cc = sc / a.SPC;
+    const int64_t cbl = (sc - cc * a.SPC) >> 6;  // column block within the chunk
+    const int64_t jt = (sc - cc * a.SPC) * TPS + kc;
     const int64_t g = cc * a.K + jt;
     const bool valid = jt < a.K && g < a.G;
     const bool live = valid && a.cnt[b][g] != 0;
-    if (t < 64) {  // active tiles of the chunk's earlier groups (comp_rms counts), wave 0
+    // tile order within the block: tile jt = (column block base) + l * TPS + kc
+    flag[l * TPS + kc] = live ? 1 : 0;
+    if (threadIdx.x < 64) {  // active tiles of the chunk's earlier column blocks (comp_rms counts), wave 0
         int32_t acc = 0;
-        const int32_t *ct = a.cbtot[b] + cc * a.GPC;
-        for (int64_t i = t; i < q; i += 64) acc += ct[i];
+        const int32_t *ct = a.cbtot[b] + cc * (a.SPC >> 6);
+        for (int64_t q = threadIdx.x; q < cbl; q += 64) acc += ct[q];
         for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-        if (t == 0) base_s = acc;
+        if (threadIdx.x == 0) base_s = acc;
     }
-    // exclusive scan of the live flags in tile order
-    const uint64_t bal = __ballot(live);
+    __syncthreads();
+    // exclusive scan of the flags in tile order: thread t takes entry t
+    const int t = threadIdx.x;
+    const bool f = flag[t] != 0;
+    const uint64_t bal = __ballot(f);
     const int wp = (int)__popcll(bal & ((1ull << (t & 63)) - 1ull));
     if ((t & 63) == 0) wsum[t >> 6] = (int32_t)__popcll(bal);
     __syncthreads();
-    int32_t r = base_s + wp;
-    for (int w = 0; w < (t >> 6); ++w) r += wsum[w];
-    if (t == RANK_GROUP - 1 && q == a.GPC - 1) a.nact[b][cc] = r + (live ? 1 : 0);  // the chunk's last group
+    int32_t woff = base_s;
+    for (int w = 0; w < (t >> 6); ++w) woff += wsum[w];
+    pre[t] = woff + wp;
+    if (t == NT - 1 && cbl == (a.SPC >> 6) - 1) a.nact[b][cc] = woff + wp + (f ? 1 : 0);  // the chunk's last block
+    __syncthreads();
+    const int32_t r = pre[l * TPS + kc];
     const int64_t ci = cc * a.K + r;
     if (valid) a.rank[b][g] = r;
     if (live) {
@@ -700,7 +718,8 @@ __device__ void compose_super(const CompArgs &a, int b, int64_t s, int64_t ci0) 
 // E - q (exact while it stays in E's binade: the offsets do not depend on M), max'ed
 // with ct (a walk that clamps ends on ct's values: the steps are monotone).  An
 // uncovered E takes E - Dt (a guess; exactness never depends on it).
-__device__ __forceinline__ double e_fold_tile(double E, double ct, double Dt, double mx, const double (&q)[2 * JB]) {
+template <typename QF>
+__device__ __forceinline__ double e_fold_tile(double E, double ct, double Dt, double mx, QF &&qat) {
     constexpr uint64_t MANT = (1ull << 52) - 1;
     if (!(E > 0.0)) return ct;
     const uint64_t ab = (uint64_t)__double_as_longlong(E);
@@ -708,11 +727,7 @@ __device__ __forceinline__ double e_fold_tile(double E, double ct, double Dt, do
     if (k < 0) return ct;
     double x = E - Dt;
     if (k < JB) {
-        const int idx = 2 * k + (int)(ab & 1);
-        double qv = q[0];
-#pragma unroll
-        for (int j = 1; j < 2 * JB; ++j) qv = idx == j ? q[j] : qv;
-        const double y = E - qv;
+        const double y = E - qat(2 * k + (int)(ab & 1));  // (qat: the record entry, loaded by index)
         const uint64_t yb = (uint64_t)__double_as_longlong(y);
         if (y == y && (yb >> 52) == (ab >> 52) && (yb & MANT) != 0) x = y;
     }
@@ -728,8 +743,14 @@ __device__ __forceinline__ double e_fold_tile(double E, double ct, double Dt, do
 constexpr int PASS0_BLOCK = 64, P0_MAXL = 64;  // lanes; tiles per walker (warm-up included)
 constexpr int E_TILES = 32;  // active tiles folded into a pass-0 guess by default (~4000 frames of release history)
 
+constexpr int EW_MAX = 64 * SJ_TPS + 64;  // tiles a pass-0 block stages for its guesses (TPS <= 4, window <= 64)
+constexpr int P0_SMEM = (EW_MAX * (3 + 2 * JB) * 8 > P0_MAXL * PASS0_BLOCK * 4) ? EW_MAX * (3 + 2 * JB) * 8
+                                                                                 : P0_MAXL * PASS0_BLOCK * 4;
+
 __global__ void __launch_bounds__(PASS0_BLOCK) comp_pass0_kernel(CompArgs a) {
-    __shared__ uint32_t offs_lds[P0_MAXL][PASS0_BLOCK];
+    // LDS: first the staged tile summaries of the guesses, then the walk's tile offsets
+    __shared__ __attribute__((aligned(16))) char smem[P0_SMEM];
+    uint32_t(*offs_lds)[PASS0_BLOCK] = reinterpret_cast<uint32_t(*)[PASS0_BLOCK]>(smem);
     const int b = blockIdx.y;
     const BandStep bs = band_step(a, b);
     const Plane p = plane(a, b, (int64_t)blockIdx.x * PASS0_BLOCK / a.SPC);  // (a block's 64 columns: one chunk)
@@ -743,6 +764,45 @@ __global__ void __launch_bounds__(PASS0_BLOCK) comp_pass0_kernel(CompArgs a) {
     const int W = min(a.warmup, 1);
     const int64_t cw0 = max(cK, st.ci0 - (int64_t)W * a.TPS);  // first compact index walked
     const int nwarm = live ? (int)(st.ci0 - cw0) : 0, ntot = live ? nwarm + st.ntiles : 0;
+    // the guess: the (max,+) walk of the e_tiles active tiles before the walk, from 0
+    // (every attack an instant clamp, release at M/R per frame): bit-exact across
+    // covered tiles, so after a loud stretch it carries the very release values a
+    // speculative walk that clamped at the same peak computes (the M of the first
+    // frame left ~all super-tiles stale).  The block's 64 windows
+    // overlap: their tiles are staged in LDS once (coalesced), then each lane folds
+    // its own window from LDS.
+    double att = 0.0;
+    {
+        const int64_t nact_c = a.nact[b][sc / a.SPC];
+        const int64_t lo = max(cK, (int64_t)__shfl(cw0, 0) - a.e_tiles);
+        const int64_t hi = min(cK + nact_c, (int64_t)__shfl(cw0, 63));
+        const int64_t n = hi - lo;
+        const bool staged = n <= EW_MAX;
+        double *sc_c = reinterpret_cast<double *>(smem);
+        double *sc_d = sc_c + EW_MAX, *sc_m = sc_d + EW_MAX, *sc_q = sc_m + EW_MAX;  // q: [2 JB][EW_MAX]
+        if (staged && n > 0) {
+            const double2 *cd = reinterpret_cast<const double2 *>(a.cedc[b]);
+            const double2 *qd = reinterpret_cast<const double2 *>(a.descc[b]);
+            for (int i = lane; i < n; i += PASS0_BLOCK) {
+                const double2 v = cd[lo + i];
+                sc_c[i] = v.x;
+                sc_d[i] = v.y;
+                sc_m[i] = a.mmaxc[b][lo + i];
+#pragma unroll
+                for (int k = 0; k < JB; ++k) {
+                    const double2 q = qd[(lo + i) * (DREC / 2) + k];
+                    sc_q[(2 * k) * EW_MAX + i] = q.x;
+                    sc_q[(2 * k + 1) * EW_MAX + i] = q.y;
+                }
+            }
+        }
+        __syncthreads();
+        if (live && cw0 != cK && staged) {  // (a larger window or super-tile than the stage holds: guess 0)
+            for (int64_t i = max(cK, cw0 - a.e_tiles) - lo; i < cw0 - lo; ++i)
+                att = e_fold_tile(att, sc_c[i], sc_d[i], sc_m[i], [&](int idx) { return sc_q[idx * EW_MAX + i]; });
+        }
+        __syncthreads();  // (the stage is reused for the walk's offsets)
+    }
     int nmax = ntot;
     for (int o = 32; o > 0; o >>= 1) nmax = max(nmax, __shfl_xor(nmax, o));
     nmax = __builtin_amdgcn_readfirstlane(nmax);
@@ -750,37 +810,6 @@ __global__ void __launch_bounds__(PASS0_BLOCK) comp_pass0_kernel(CompArgs a) {
     for (int i = 0; i < nmax; ++i)  // the walk's tile offsets (lanes past their own repeat their last)
         offs_lds[i][lane] = tile_off(a, ntot ? tl[cw0 + min(i, ntot - 1)] : 0);
     __syncthreads();
-    // the guess: the (max,+) walk of the E_TILES active tiles before the walk, from 0
-    // (every attack an instant clamp, release at M/R per frame): bit-exact across
-    // covered tiles, so after a loud stretch it carries the very release values a
-    // speculative walk that clamped at the same peak computes (the M of the first
-    // frame left ~all super-tiles stale)
-    double att = 0.0;
-    if (live && cw0 != cK) {
-        const double2 *cd = reinterpret_cast<const double2 *>(a.cedc[b]);
-        const double *mxc = a.mmaxc[b];
-        const double2 *qd = reinterpret_cast<const double2 *>(a.descc[b]);
-        constexpr int EG = 4;  // tiles per load group
-        for (int64_t i = max(cK, cw0 - a.e_tiles); i < cw0; i += EG) {
-            double2 cdv[EG];
-            double mxv[EG], qv[EG][2 * JB];
-#pragma unroll
-            for (int t = 0; t < EG; ++t) {
-                const int64_t it = min(i + t, cw0 - 1);
-                cdv[t] = cd[it];
-                mxv[t] = mxc[it];
-#pragma unroll
-                for (int k = 0; k < JB; ++k) {
-                    const double2 v = qd[it * (DREC / 2) + k];
-                    qv[t][2 * k] = v.x;
-                    qv[t][2 * k + 1] = v.y;
-                }
-            }
-#pragma unroll
-            for (int t = 0; t < EG; ++t)
-                if (i + t < cw0) att = e_fold_tile(att, cdv[t].x, cdv[t].y, mxv[t], qv[t]);
-        }
-    }
     if (a.sjump) {  // the super-tile's release-jump record (the sweeps' super jumps)
         if (live && st.ntiles == SJ_TPS && a.TPS == SJ_TPS) compose_super(a, b, s, st.ci0);
         else if (s < a.GS) a.se0[b][s] = SJ_NONE;
@@ -946,12 +975,11 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
         if (++ci < ce) return true;
         st_sc1(end + cur, att);
         if (st.last) return false;  // the chunk's last super-tile
-        // the Jacobi sweep stops here (its walkers are every stale super-tile: a chain
-        // through a successor would run behind it; the successor is stale next sweep,
-        // which this walk's own `changed` flag queues); run-head sweeps continue if the
-        // successor could be claimed (else its owner read an older end of cur: stale
-        // next sweep)
-        if (!a.heads && !a.jacobi_continue) return false;
+        // continue into the successor if it could be claimed (else its owner read an
+        // older end of cur: it is stale next sweep, which this walk's own `changed`
+        // flag queues); with jacobi_stop the Jacobi sweep's walkers stop here instead
+        // (C2: 5 sweeps, fix 0.295 ms against 3 and 0.269 continuing)
+        if (!a.heads && a.jacobi_stop) return false;
         if (!a.heads) nx_claimed = comp_claim(a, b, cur + 1);
         if (!nx_claimed) return false;
         ++cur;
@@ -1043,7 +1071,7 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
             w.i0 = 0;
             w.nst = 1;
             const uint32_t off = tile_off(a, m.g);
-            stream_col<true, WNB>(p, [&](int) { return off; }, 1, a.TP, w);  // (the walking lanes step the same rows)
+            stream_col<true, FIX_WNB>(p, [&](int) { return off; }, 1, a.TP, w);  // (the walking lanes step the same rows)
             att = w.att;
             walked += T;
             walk = false;

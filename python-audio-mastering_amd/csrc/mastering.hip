@@ -433,7 +433,7 @@ static int solve_geometry(const mm_job *j, mm_solve_geom *g) {
     if (K < 1 || T < 1 || j->frames_proc < 0) return MM_ERR_ARG;
     const int64_t G = (j->frames_proc + T - 1) / T;
     *g = mm_solve_geom{};
-    g->tps = std::max(1, std::min((j->comp_super + T / 2) / T, P0_MAXL / 2));  // (a walk plus a warm-up super-tile)
+    g->tps = std::max(1, std::min((j->comp_super + T / 2) / T, DESC_MAX_TPS));  // (comp_describe: 64 TPS threads)
     g->chunks = (G + K - 1) / K;
     g->cols_per_chunk = (((int64_t)K + g->tps - 1) / g->tps + 63) / 64 * 64;
     g->tile_rows = (T + WB - 1) / WB * WB;
@@ -490,7 +490,6 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     const int64_t nchunks = sg.chunks;
     ca.TPS = sg.tps;
     ca.SPC = sg.cols_per_chunk;
-    ca.GPC = ((int64_t)K + RANK_GROUP - 1) / RANK_GROUP;
     ca.GS = nchunks * ca.SPC;
     const int64_t NS = ca.GS;
     short2 *q2;
@@ -516,7 +515,7 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     RET(get_buf(c, "comp_nact", (size_t)3 * nchunks, &nacts));
     ca.jumps = getenv("MM_COMP_NOJUMP") ? 0 : 1;  // diagnostics: results must not change
     ca.sjump = ca.jumps && !getenv("MM_COMP_NOSJUMP") && ca.TPS == SJ_TPS ? 1 : 0;
-    ca.jacobi_continue = getenv("MM_JACOBI_CONTINUE") ? 1 : 0;  // (tuning experiments)
+    ca.jacobi_stop = getenv("MM_JACOBI_STOP") ? 1 : 0;  // (tuning experiments)
     ca.e_tiles = E_TILES;
     if (const char *e = getenv("MM_E_TILES")) ca.e_tiles = std::max(0, atoi(e));  // (tuning experiments)
     double *sdesc;
@@ -578,12 +577,10 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
         ca.claim[b] = claims + (size_t)b * NS;
         ca.sdesc[b] = ca.sjump ? sdesc + (size_t)b * NS * SREC : nullptr;
         ca.se0[b] = ca.sjump ? se0s + (size_t)b * NS : nullptr;
-        ca.cbtot[b] = reinterpret_cast<int32_t *>(claims + (size_t)3 * NS) + (size_t)b * nchunks * ca.GPC;
+        ca.cbtot[b] = reinterpret_cast<int32_t *>(claims + (size_t)3 * NS) + (size_t)b * (NS / 64);
     }
-    const int64_t WPC = ((int64_t)K + 63) / 64;  // comp_rms / comp_apply waves (blocks) per chunk
-    RET(launch(c, "comp_rms", comp_rms_kernel, dim3(blocks_for(nchunks * WPC, 4), 3), dim3(256), 0, ca));
-    RET(launch(c, "comp_describe", comp_describe_kernel, dim3((unsigned)(nchunks * ca.GPC), 3), dim3(RANK_GROUP), 0,
-               ca));
+    RET(launch(c, "comp_rms", comp_rms_kernel, dim3(blocks_for(NS / 64 * ca.TPS, 4), 3), dim3(256), 0, ca));
+    RET(launch(c, "comp_describe", comp_describe_kernel, dim3((unsigned)(NS / 64), 3), dim3(64 * ca.TPS), 0, ca));
     RET(launch(c, "comp_pass0", comp_pass0_kernel, dim3(blocks_for(NS, PASS0_BLOCK), 3), dim3(PASS0_BLOCK), 0, ca));
     c->comp_on = true;
     c->ca = ca;
@@ -621,7 +618,7 @@ static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
         nch = sg.chunks;
         spc = sg.cols_per_chunk;
     }
-    RET(setup_control(c, nblk, nch, 3 * nch * spc + 3 * nch * ((K + RANK_GROUP - 1) / RANK_GROUP)));  // claim stamps, group counts
+    RET(setup_control(c, nblk, nch, 3 * nch * spc + 3 * nch * spc / 64));  // claim stamps, column-block counts
 
     EqArgs ea{};
     ea.in = j->in_kind == MM_IN_I16 ? nullptr : static_cast<const float *>(d_in);

@@ -557,8 +557,7 @@ int mm_op_compress_bands(mm_ctx *c, const mm_job *j, const int16_t *lo, const in
     c->staged = false;
     mm_solve_geom sg;
     solve_geometry(j, &sg);  // (checked by stage_compress)
-    RET(setup_control(c, blocks_for(G, LB_THREADS / ch), sg.chunks,
-                      3 * sg.chunks * (sg.cols_per_chunk + (j->tiles_per_chunk + RANK_GROUP - 1) / RANK_GROUP)));
+    RET(setup_control(c, blocks_for(G, LB_THREADS / ch), sg.chunks, 3 * sg.chunks * sg.cols_per_chunk * 65 / 64));
     const size_t bytes = (size_t)N * ch * 2;
     char *din;
     RET(get_buf(c, "host_in", 3 * bytes, &din));
