@@ -309,7 +309,7 @@ __device__ __forceinline__ double comp_step(double att, double M, const BandStep
     return att <= M ? up : dn;
 }
 
-// v_min_f64 / v_max_f64 without the operand canonicalisation fmin/fmax add
+// v_min_f64 without the operand canonicalisation fmin adds
 // (operands here are never NaN; equal operands and signed zeros give the same
 // observable att)
 __device__ __forceinline__ double vmin(double x, double y) {
@@ -317,16 +317,13 @@ __device__ __forceinline__ double vmin(double x, double y) {
     asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
     return r;
 }
-__device__ __forceinline__ double vmax0(double x) {
-    double r;
-    asm("v_max_f64 %0, %1, 0" : "=v"(r) : "v"(x));
-    return r;
-}
 
-// the step given M and its (precomputed) increments
+// the step given M and its (precomputed) increments.  The release branch needs no
+// max(., 0): it is taken for att > m, and dec = RN(m/R) <= m (R >= 1, checked on
+// the host), so att - dec > 0 and its rounding is >= 0 (pydub's max is the identity)
 __device__ __forceinline__ double lean_step(double att, double m, double inc, double dec) {
     const double up = vmin(att + inc, m);
-    const double dn = vmax0(att - dec);
+    const double dn = att - dec;
     return att <= m ? up : dn;
 }
 

@@ -80,19 +80,6 @@ __device__ __forceinline__ double df2t(double x, double &z0, double &z1, const d
 #define MM_KW_NB 3
 #endif
 constexpr int EQ_STAGE = MM_EQ_STAGE;  // frames per tile staged through LDS per step
-#ifndef MM_P1_DOT
-#define MM_P1_DOT 1
-#endif
-// Pass 1 of a full tile forms its zero-state end state as the dot product with the
-// stage's state response (LbArgs::resp, 8 FMAs per frame with the coefficients in
-// SGPRs: the frame index is uniform) instead of stepping the sections (EQ 20, the
-// crossover 20 VALU per frame).  It only feeds the look-back carry, which pass 2
-// then runs from in scipy's operation order.
-__device__ __forceinline__ void resp_acc(const double *resp, int n, double x, double (&acc)[8]) {
-    const double *r = resp + (size_t)__builtin_amdgcn_readfirstlane(n) * 8;
-#pragma unroll
-    for (int d = 0; d < 8; ++d) acc[d] = fma(r[d], x, acc[d]);
-}
 
 struct EqArgs {
     const float *in;   // natural interleaved f32 input (or null when in16 is set)
@@ -123,11 +110,7 @@ constexpr int eq_lds_bytes() {
 // threads read one tile's 128 contiguous bytes), double-buffered so the next
 // stage's loads are in flight while lanes run the recurrence.
 template <int NS, int CH, bool P2, bool I16>
-__device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, double (&z)[NS][2], float *stage,
-                        const double *resp = nullptr) {
-    // pass 1 of a full tile: the end state by the state response (resp_acc)
-    const bool dot = !P2 && MM_P1_DOT && resp != nullptr && len == a.T;
-    double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+__device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, double (&z)[NS][2], float *stage) {
     constexpr int TPB = LB_THREADS / CH;
     constexpr int ROW = (EQ_STAGE + 1) * CH;       // floats per staged tile row (padded)
     constexpr int ITEMS = TPB * EQ_STAGE / LB_THREADS;  // frames each thread loads per step
@@ -189,10 +172,6 @@ __device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, doub
             if (a.sat.on) x = saturate(x, a.sat);
             if (!P2) a.xs[((int64_t)n * a.G + g0 + t) * CH + c] = x;  // pass 2 reads it back coalesced
             double y = (double)x;
-            if (!P2 && dot) {
-                resp_acc(resp, n, y, acc);
-                continue;
-            }
 #pragma unroll
             for (int s = 0; s < NS; ++s) y = df2t<P2>(y, z[s][0], z[s][1], sos[s]);
             if (P2) {
@@ -210,13 +189,6 @@ __device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, doub
         }
         if (step + 1 < nsteps) store(cur ^ 1);
         lds_barrier();
-    }
-    if (dot) {
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            z[s][0] = acc[2 * s];
-            z[s][1] = acc[2 * s + 1];
-        }
     }
 }
 
@@ -272,7 +244,7 @@ __global__ void __launch_bounds__(LB_THREADS, 4) eq_kernel(EqArgs a, LbArgs lb, 
     double zs[NS][2];
 #pragma unroll
     for (int s = 0; s < NS; ++s) zs[s][0] = zs[s][1] = 0.0;
-    eq_pass<NS, CH, false, I16>(a, g0, t, c, len, zs, stage, lb.resp);
+    eq_pass<NS, CH, false, I16>(a, g0, t, c, len, zs, stage);
     double z[DIM], s[DIM], rst[DIM];
 #pragma unroll
     for (int s_ = 0; s_ < NS; ++s_) {
@@ -398,26 +370,6 @@ __device__ __forceinline__ void xo_pass(const XoArgs &a, int64_t g, int c, int l
     }
 }
 
-// pass 1 of a full crossover tile: the end state by the state response (resp_acc)
-template <int CH>
-__device__ __forceinline__ void xo_pass1_dot(const XoArgs &a, const double *resp, int64_t g, int c, double (&z)[4][2]) {
-    const int64_t G = a.G;
-    const int T = a.T;
-    double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    int n = 0;
-    stream<8, MM_XO_NB, int16_t>(
-        T, [&](int i) { return a.q_in[((int64_t)min(i, T - 1) * G + g) * 2 + c]; },
-        [&](int16_t q) {
-            resp_acc(resp, n, (double)((float)q / 32768.0f), acc);  // AME:199 int16 -> f32
-            ++n;
-        });
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        z[k][0] = acc[2 * k];
-        z[k][1] = acc[2 * k + 1];
-    }
-}
-
 template <int CH>
 __global__ void __launch_bounds__(LB_THREADS, 4) xover_kernel(XoArgs a, LbArgs lb, int64_t line_tiles) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -431,10 +383,7 @@ __global__ void __launch_bounds__(LB_THREADS, 4) xover_kernel(XoArgs a, LbArgs l
     const bool valid = g < a.G;
     const int len = valid ? (int)min((int64_t)a.T, a.N_proc - g * a.T) : 0;
     double zs[4][2] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
-    if (valid) {
-        if (MM_P1_DOT && lb.resp && len == a.T) xo_pass1_dot<CH>(a, lb.resp, g, c, zs);
-        else xo_pass<CH, false>(a, g, c, len, zs);
-    }
+    if (valid) xo_pass<CH, false>(a, g, c, len, zs);
     double z[8], s[8], rst[8];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {

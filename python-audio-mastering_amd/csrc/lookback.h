@@ -47,7 +47,6 @@ struct LbArgs {
     unsigned *error;        // [1]      set to 1 on a spin timeout
     const double *init;     // [CH][8]  state at the track start (or null = 0)
     int64_t line_tiles;     // line starts at tiles g % line_tiles == 0
-    const double *resp;     // [T][8] state response: end state of a zero-state tile = sum_n resp[n] x_n
 };
 
 typedef __attribute__((address_space(1))) unsigned gu32;

@@ -188,45 +188,12 @@ static void resolve_events(mm_ctx *c) {
 static inline unsigned blocks_for(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
 
 // ------------------------------------------------------- look-back plumbing
-// State response of a zero-state tile of T frames to its inputs: the end state is
-// sum_n R[n] x_n with R[n] = A^(T-1-n) B (the stage's DF2T sections, branch 0 of
-// nsec_branch0 sections and branch 1 of the rest, both fed by x; state (z0, z1) per
-// section in section order, padded to 8).  Pass 1 of the IIR kernels forms the
-// tile's end state as this dot product (8 FMAs per frame, the coefficients in
-// SGPRs) instead of stepping the sections; it only feeds the look-back carry.
-static void state_response(const mm_iir &f, int T, double *R) {
-    const int ns = f.nsec;
-    double z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    std::vector<double> S((size_t)T * 8);
-    for (int m = 0; m < T; ++m) {  // impulse at frame 0
-        const double x = m == 0 ? 1.0 : 0.0;
-        double nz[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        int s = 0;
-        for (int br = 0; br < 2 && s < ns; ++br) {
-            const int nb = br == 0 ? (f.nsec_branch0 > 0 ? f.nsec_branch0 : ns) : ns - s;
-            double xs = x;
-            for (int k = 0; k < nb; ++k, ++s) {
-                const double *c = f.sos[s];
-                const double y = c[0] * xs + z[2 * s];
-                nz[2 * s] = c[1] * xs - c[3] * y + z[2 * s + 1];
-                nz[2 * s + 1] = c[2] * xs - c[4] * y;
-                xs = y;
-            }
-        }
-        memcpy(z, nz, sizeof z);
-        memcpy(&S[(size_t)m * 8], z, sizeof z);  // the state m + 1 steps after the impulse
-    }
-    for (int n = 0; n < T; ++n) memcpy(R + (size_t)n * 8, &S[(size_t)(T - 1 - n) * 8], 8 * sizeof(double));
-}
-
 // Transition tables of one filter stage (uploaded only when they change).
 static int upload_tables(mm_ctx *c, const char *name, const mm_iir &f, LbArgs &lb) {
-    const size_t nt = (size_t)(MM_TILE_POW + MM_BLK_POW) * 64, T = (size_t)std::max(f.tile, 1);
-    const size_t n = nt + T * 8;
+    const size_t n = (size_t)(MM_TILE_POW + MM_BLK_POW) * 64;
     std::vector<double> host(n);
     memcpy(host.data(), f.phi_tile_pow, sizeof f.phi_tile_pow);
     memcpy(host.data() + MM_TILE_POW * 64, f.phi_blk_pow, sizeof f.phi_blk_pow);
-    state_response(f, (int)T, host.data() + nt);
     const std::string key = std::string("tab_") + name;
     double *d;
     RET(get_buf(c, key.c_str(), n, &d));
@@ -238,7 +205,6 @@ static int upload_tables(mm_ctx *c, const char *name, const mm_iir &f, LbArgs &l
     }
     lb.pw_tile = d;
     lb.pw_blk = d + MM_TILE_POW * 64;
-    lb.resp = d + nt;
     return MM_OK;
 }
 
