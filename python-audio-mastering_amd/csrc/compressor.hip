@@ -504,7 +504,10 @@ struct Walker {
 //   x >= 2^e + u (every exact difference a_k - d_k >= a_{k+1} - u/2 > 2^e: grid u)
 // and then lands EXACTLY on the state the step-by-step walk reaches.  Inactive
 // frames (M = 0) are d = 0 steps for both.
-constexpr int JB = 4;  // binades per descriptor: e0 .. e0 + JB - 1
+#ifndef MM_JB
+#define MM_JB 4
+#endif
+constexpr int JB = MM_JB;  // binades per descriptor: e0 .. e0 + JB - 1
 struct SegDesc {
     double mx;
     int e0;

@@ -170,7 +170,9 @@ __device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, doub
             if (n >= len) break;
             float x = row[j * CH + c];
             if (a.sat.on) x = saturate(x, a.sat);
+#ifndef MM_EQ_RECOMPUTE
             if (!P2) a.xs[((int64_t)n * a.G + g0 + t) * CH + c] = x;  // pass 2 reads it back coalesced
+#endif
             double y = (double)x;
 #pragma unroll
             for (int s = 0; s < NS; ++s) y = df2t<P2>(y, z[s][0], z[s][1], sos[s]);
@@ -260,7 +262,11 @@ __global__ void __launch_bounds__(LB_THREADS, 4) eq_kernel(EqArgs a, LbArgs lb, 
         zs[s_][0] = s[2 * s_];
         zs[s_][1] = s[2 * s_ + 1];
     }
+#ifdef MM_EQ_RECOMPUTE  // pass 2 re-stages the input and recomputes the exciter (no scratch)
+    eq_pass<NS, CH, true, I16>(a, g0, t, c, len, zs, stage);
+#else
     if (valid) eq_pass2<NS, CH>(a, g, c, len, zs);
+#endif
 }
 
 // No active EQ stage: the chain stays f32 (AME:152-162 returns the f32 input;

@@ -20,3 +20,10 @@ for k in range(16):
     print(f"sweep {k}: {len(r)} walkers, max {t_us.max():.1f} us, walked {int(r[:, 1].sum())} jumped {int(r[:, 2].sum())} "
           f"visited {int(r[:, 3].sum())}; fit us = {coef[0]:.3f}*walked + {coef[1]:.3f}*jumped + {coef[2]:.3f}*visited + "
           f"{coef[3]:.2f}")
+    top = np.argsort(-t_us)[:6]
+    print("   longest walkers (us, walked, jumped, visited):",
+          "; ".join(f"{t_us[i]:.1f} {int(r[i, 1])} {int(r[i, 2])} {int(r[i, 3])}" for i in top))
+    one = (r[:, 3] == 1) & (r[:, 1] == 0) & (r[:, 2] == 0)
+    if one.any():
+        print(f"   walkers that stop at once (coalesced on entry): {int(one.sum())}, median {np.median(t_us[one]):.1f} us, "
+              f"max {t_us[one].max():.1f} us")
