@@ -505,9 +505,10 @@ struct Walker {
 // and then lands EXACTLY on the state the step-by-step walk reaches.  Inactive
 // frames (M = 0) are d = 0 steps for both.
 #ifndef MM_JB
-#define MM_JB 4
+#define MM_JB 8
 #endif
 constexpr int JB = MM_JB;  // binades per descriptor: e0 .. e0 + JB - 1
+constexpr int JF = JB < 4 ? JB : 4;  // binades of the records the pass-0 guess folds use (e_fold_tile)
 struct SegDesc {
     double mx;
     int e0;
@@ -582,7 +583,7 @@ struct Describer {
 #ifndef MM_DESC_NB
 #define MM_DESC_NB 1
 #endif
-constexpr int DESC_MAX_TPS = 16;  // block = 64 * TPS <= 1024 threads
+constexpr int DESC_MAX_TPS = 8;  // block = 64 * TPS <= 512 threads (tile rounding: TPS = round(500 / T) <= 8)
 
 __global__ void __launch_bounds__(64 * DESC_MAX_TPS) comp_describe_kernel(CompArgs a) {
     __shared__ int32_t wsum[DESC_MAX_TPS], base_s;
@@ -682,9 +683,10 @@ __device__ void compose_super(const CompArgs &a, int b, int64_t s, int64_t ci0) 
 #pragma unroll
     for (int t = 0; t < SJ_TPS; ++t) mxs = fmax(mxs, mxt[t]);
     const int e0s = binade(mxs);
-    double rec[SREC];
+    double *out = a.sdesc[b] + s * SREC;
 #pragma unroll
     for (int k = 0; k < 2 * JB; ++k) {
+        double rec[SJ_ENT];
         double Q = 0.0, L = 0.0;
         int par = k & 1;
         bool ok = true;
@@ -701,13 +703,12 @@ __device__ void compose_super(const CompArgs &a, int b, int64_t s, int64_t ci0) 
             ok = ok && Q < ldexp(1.0, e);
             if (ok) par ^= (int)((int64_t)ldexp(qv, 52 - e) & 1);  // qv / u, an exact integer
             L = fmax(L, next_up(mxt[t] + Q));
-            rec[k * SJ_ENT + 1 + t] = Q;
+            rec[1 + t] = Q;
         }
-        rec[k * SJ_ENT] = ok ? L : __longlong_as_double(0x7ff8000000000000ll);
-    }
-    double2 *out = reinterpret_cast<double2 *>(a.sdesc[b] + s * SREC);
+        rec[0] = ok ? L : __longlong_as_double(0x7ff8000000000000ll);
 #pragma unroll
-    for (int k = 0; k < SREC / 2; ++k) out[k] = make_double2(rec[2 * k], rec[2 * k + 1]);
+        for (int j = 0; j < SJ_ENT; ++j) out[k * SJ_ENT + j] = rec[j];  // (entry k: its own stores)
+    }
     a.se0[b][s] = e0s;
 }
 
@@ -726,7 +727,7 @@ __device__ __forceinline__ double e_fold_tile(double E, double ct, double Dt, do
     const int k = (int)(ab >> 52) - 1023 - binade(mx);
     if (k < 0) return ct;
     double x = E - Dt;
-    if (k < JB) {
+    if (k < JF) {
         const double y = E - qat(2 * k + (int)(ab & 1));  // (qat: the record entry, loaded by index)
         const uint64_t yb = (uint64_t)__double_as_longlong(y);
         if (y == y && (yb >> 52) == (ab >> 52) && (yb & MANT) != 0) x = y;
@@ -744,7 +745,7 @@ constexpr int PASS0_BLOCK = 64, P0_MAXL = 64;  // lanes; tiles per walker (warm-
 constexpr int E_TILES = 32;  // active tiles folded into a pass-0 guess by default (~4000 frames of release history)
 
 constexpr int EW_MAX = 64 * SJ_TPS + 64;  // tiles a pass-0 block stages for its guesses (TPS <= 4, window <= 64)
-constexpr int P0_SMEM = (EW_MAX * (3 + 2 * JB) * 8 > P0_MAXL * PASS0_BLOCK * 4) ? EW_MAX * (3 + 2 * JB) * 8
+constexpr int P0_SMEM = (EW_MAX * (3 + 2 * JF) * 8 > P0_MAXL * PASS0_BLOCK * 4) ? EW_MAX * (3 + 2 * JF) * 8
                                                                                  : P0_MAXL * PASS0_BLOCK * 4;
 
 __global__ void __launch_bounds__(PASS0_BLOCK) comp_pass0_kernel(CompArgs a) {
@@ -779,7 +780,7 @@ __global__ void __launch_bounds__(PASS0_BLOCK) comp_pass0_kernel(CompArgs a) {
         const int64_t n = hi - lo;
         const bool staged = n <= EW_MAX;
         double *sc_c = reinterpret_cast<double *>(smem);
-        double *sc_d = sc_c + EW_MAX, *sc_m = sc_d + EW_MAX, *sc_q = sc_m + EW_MAX;  // q: [2 JB][EW_MAX]
+        double *sc_d = sc_c + EW_MAX, *sc_m = sc_d + EW_MAX, *sc_q = sc_m + EW_MAX;  // q: [2 JF][EW_MAX]
         if (staged && n > 0) {
             const double2 *cd = reinterpret_cast<const double2 *>(a.cedc[b]);
             const double2 *qd = reinterpret_cast<const double2 *>(a.descc[b]);
@@ -789,7 +790,7 @@ __global__ void __launch_bounds__(PASS0_BLOCK) comp_pass0_kernel(CompArgs a) {
                 sc_d[i] = v.y;
                 sc_m[i] = a.mmaxc[b][lo + i];
 #pragma unroll
-                for (int k = 0; k < JB; ++k) {
+                for (int k = 0; k < JF; ++k) {
                     const double2 q = qd[(lo + i) * (DREC / 2) + k];
                     sc_q[(2 * k) * EW_MAX + i] = q.x;
                     sc_q[(2 * k + 1) * EW_MAX + i] = q.y;
