@@ -114,7 +114,10 @@ __device__ __forceinline__ double *chunk_plane(const CompArgs &a, int b, int64_t
 // (identity steps).  Also the tile's active count and largest M (the table is
 // nondecreasing in r), its (max,+) release summary for the pass-0 guesses, and the
 // per-chunk active count.
-__global__ void __launch_bounds__(256) comp_rms_kernel(CompArgs a) {
+#ifndef MM_RMS_MINB
+#define MM_RMS_MINB 1
+#endif
+__global__ void __launch_bounds__(256, MM_RMS_MINB) comp_rms_kernel(CompArgs a) {
     const int b = blockIdx.y;
     const int64_t wv = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int kc = (int)(wv % a.TPS);
@@ -341,15 +344,18 @@ struct Super {
     bool last;    // the chunk's last non-empty one
 };
 
-__device__ __forceinline__ Super super_of(const CompArgs &a, int b, int64_t s) {
+// (na: the chunk's active tiles, a.nact)
+__device__ __forceinline__ Super super_of_na(const CompArgs &a, int64_t s, int na) {
     Super r;
     const int64_t c = s / a.SPC, j = s - c * a.SPC;
-    const int na = a.nact[b][c];
     r.ci0 = c * a.K + j * a.TPS;
     r.ntiles = (int)max((int64_t)0, min((int64_t)a.TPS, (int64_t)na - j * a.TPS));
     r.first = j == 0;
     r.last = (j + 1) * a.TPS >= na;
     return r;
+}
+__device__ __forceinline__ Super super_of(const CompArgs &a, int b, int64_t s) {
+    return super_of_na(a, s, a.nact[b][s / a.SPC]);
 }
 
 #ifndef MM_WALK_B
@@ -657,7 +663,11 @@ __global__ void __launch_bounds__(64 * DESC_MAX_TPS) comp_describe_kernel(CompAr
 // tools/study/envelope_model.c), with the next record prefetched.
 constexpr int SJ_TPS = 4;               // tiles per super-tile with records
 constexpr int SJ_ENT = SJ_TPS + 1;      // doubles per (kb, p) entry: L, Q[1..SJ_TPS]
-constexpr int SREC = 2 * JB * SJ_ENT;   // doubles per super-tile record
+#ifndef MM_SJB
+#define MM_SJB 4
+#endif
+constexpr int SJB = MM_SJB < JB ? MM_SJB : JB;  // binades per super-tile record: e0s .. e0s + SJB - 1
+constexpr int SREC = 2 * SJB * SJ_ENT;  // doubles per super-tile record
 constexpr int SJ_NONE = -100000;        // se0 of a super-tile without a record
 
 __device__ __forceinline__ double next_up(double x) {
@@ -685,7 +695,7 @@ __device__ void compose_super(const CompArgs &a, int b, int64_t s, int64_t ci0) 
     const int e0s = binade(mxs);
     double *out = a.sdesc[b] + s * SREC;
 #pragma unroll
-    for (int k = 0; k < 2 * JB; ++k) {
+    for (int k = 0; k < 2 * SJB; ++k) {
         double rec[SJ_ENT];
         double Q = 0.0, L = 0.0;
         int par = k & 1;
@@ -880,7 +890,8 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
     const int64_t s = (int64_t)blockIdx.x * 64 + threadIdx.x;
     const int b = blockIdx.y;
     if (s >= a.GS) return;
-    Super st = super_of(a, b, s);
+    const int na_c = a.nact[b][s / a.SPC];  // (a walk stays in its chunk)
+    Super st = super_of_na(a, s, na_c);
     if (st.ntiles == 0 || st.first) return;  // chunk starts are exact
     double *end = a.end[b];
     double att = ld_sc1(end + s - 1);
@@ -897,7 +908,7 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
     double *tst = a.tstc[b];
     const int T = a.T;
     int64_t walked = 0, jumped = 0;
-    const int64_t cend = st.ci0 + (int64_t)(a.nact[b][s / a.SPC]) - (s % a.SPC) * a.TPS;  // past the chunk's last
+    const int64_t cend = st.ci0 + (int64_t)na_c - (s % a.SPC) * a.TPS;  // past the chunk's last
     auto ld = [&](int64_t ci) __attribute__((always_inline)) {
         TileMeta m;
         ci = min(ci, cend - 1);
@@ -929,7 +940,7 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
     double old_c = 0.0, old_n = 0.0;      // stored entry states of cur's, cur + 1's first tile
     double ec[2][SJ_ENT], en[2][SJ_ENT];  // entries (parity 0, 1) of cur, cur + 1
     auto ld_ent = [&](int64_t sx, int kb, double (&e)[2][SJ_ENT]) __attribute__((always_inline)) {
-        const double *r = srec + min(sx, slast) * SREC + 2 * min(max(kb, 0), JB - 1) * SJ_ENT;
+        const double *r = srec + min(sx, slast) * SREC + 2 * min(max(kb, 0), SJB - 1) * SJ_ENT;
 #pragma unroll
         for (int q = 0; q < 2; ++q)
 #pragma unroll
@@ -984,7 +995,7 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
         if (!a.heads) nx_claimed = comp_claim(a, b, cur + 1);
         if (!nx_claimed) return false;
         ++cur;
-        st = super_of(a, b, cur);
+        st = super_of_na(a, cur, na_c);
         a.start[b][cur] = att;
         ce = st.ci0 + st.ntiles;
         nx_claimed = a.heads && !st.last ? comp_claim(a, b, cur + 1) : false;
@@ -1013,7 +1024,7 @@ __global__ void __launch_bounds__(64) comp_fix_kernel(CompArgs a, const unsigned
                 constexpr uint64_t MANT = (1ull << 52) - 1;
                 const uint64_t ab = (uint64_t)__double_as_longlong(att);
                 const int kb = (int)(ab >> 52) - 1023 - e0_c;
-                if (att > 0.0 && kb >= 0 && kb < JB) {
+                if (att > 0.0 && kb >= 0 && kb < SJB) {
                     if (kb != kb_c) {  // the state left the prefetched binade
                         kb_c = kb;
                         ld_ent(cur, kb, ec);

@@ -26,7 +26,8 @@ import scipy.signal
 
 MAX_DIM = 8
 CHUNK_MS = 30 * 1000  # AME:48
-DEFAULT_TILE = 125     # divides 30 s chunks at every rate that is a multiple of 25 Hz
+DEFAULT_TILE = 225     # divides 30 s chunks at 11.025/22.05/44.1/48/88.2/96/192 kHz (round 4: T 75-250 swept,
+                       # 225 fastest on C2, P_HOT, C3 and C5)
 OPS_TILE = 125         # tile of the per-stage operators' look-back tables (== OPS_TILE in csrc/ops.hip)
 
 EQ_KEYS = ("bass_boost", "mid_cut", "presence_boost", "treble_boost")
@@ -85,14 +86,18 @@ def check_chunk_geometry(bounds, nominal: int, rate: int, multiband: bool):
 
 
 def choose_tile(chunk_frames: int, preferred: int | None = None) -> int:
+    """The tile length of a chunk: `preferred` (DEFAULT_TILE) when it divides the chunk,
+    else the divisor in [64, 512] nearest to it, counting the walk-block padding of the
+    compressor's plane rows (tiles are padded to whole 25-row blocks) as distance."""
     preferred = preferred or DEFAULT_TILE
     if chunk_frames % preferred == 0:
         return preferred
-    best = 0
-    for t in range(512, 63, -1):
+    best, best_cost = 0, None
+    for t in range(64, 513):
         if chunk_frames % t == 0:
-            best = t
-            break
+            cost = abs(t - preferred) / preferred + ((t + 24) // 25 * 25 - t) / t
+            if best_cost is None or cost < best_cost:
+                best, best_cost = t, cost
     if not best:
         raise NotImplementedError(
             f"no tile length in [64, 512] divides the {chunk_frames}-frame chunk; rate unsupported")

@@ -31,17 +31,18 @@ EQ_PRESETS = {
 
 COMP_WARMUP = 0  # super-tiles of speculative warm-up walk before each one (none: the sweeps' jumps repair starts)
 COMP_MAX_ITERS = 100000
-# envelope solve unit in frames, at EVERY rate: 4 tiles of 125.  Not scaled with the
-# rate (comp_rms maps a wave to one tile position of 64 super-tiles, so its M stores
-# are 512-byte runs at any length; shorter walks halve pass 0, and with the (max,+)
-# pass-0 guesses the sweeps barely lengthen: tools/study/envelope_model.c).
-COMP_SUPER_FRAMES = 500
+# envelope solve unit: super-tiles of 4 tiles (900 frames at the default tile) at
+# EVERY rate, the tile count the super-tile release records assume (SJ_TPS in
+# csrc/compressor.hip).  Not scaled with the rate (comp_rms maps a wave to one tile
+# position of 64 super-tiles, so its M stores are 512-byte runs at any length).
+COMP_SUPER_FRAMES = 900
 
 
 def comp_super_frames(rate: int, tile: int = design.DEFAULT_TILE) -> int:
-    """Super-tile length in frames: whole tiles (4 x 125 at every rate)."""
+    """Super-tile length in frames: COMP_SUPER_FRAMES / DEFAULT_TILE (4) whole tiles of
+    the track's tile at every rate."""
     del rate  # (see COMP_SUPER_FRAMES)
-    return max(1, int(round(COMP_SUPER_FRAMES / tile))) * tile
+    return max(1, int(round(COMP_SUPER_FRAMES / design.DEFAULT_TILE))) * tile
 
 
 class Job:

@@ -31,7 +31,7 @@ def test_c2_profile_covers_every_kernel():
     with open(os.path.join(ROOT, "profiles", f"{bench.PROFILE_ROUND}_C2_pmc_summary.json")) as f:
         prof = json.load(f)
     # every chain kernel of the C2 bench has counters and a limiter
-    for k in ("eq", "xover", "comp_rms", "comp_links", "comp_describe", "comp_pass0", "comp_fix", "comp_apply", "kweight",
+    for k in ("eq", "xover", "comp_rms", "comp_describe", "comp_pass0", "comp_fix", "comp_apply", "kweight",
               "finalize"):
         assert prof["kernels"][k]["bytes_per_launch"] > 0 and prof["kernels"][k]["limiter"], k
 
