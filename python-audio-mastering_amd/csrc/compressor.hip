@@ -45,15 +45,22 @@
 namespace mm {
 
 // x^2 + y^2 of one frame: at most 2 * 32768^2 = 2^31, exact in uint32
+template <bool V>
+struct BoolTag {
+    static constexpr bool value = V;
+};
+
 __device__ __forceinline__ uint32_t frame_energy(short2 v) {
     return (uint32_t)((int32_t)v.x * v.x) + (uint32_t)((int32_t)v.y * v.y);
 }
 
 // largest r with n*r*r <= S (== isqrt(S div n) == trunc(sqrt(S/n)) computed in
 // doubles, tests/test_oracle.py).  S and n*r*r are integers below 2^53, so the
-// f64 products and compares are exact; the f32 estimate is within 1 of r.
+// f64 products and compares are exact.  The f32 estimate (v_sqrt_f32 of S * 1/n, a
+// few ulp relative: < 0.01 absolute at r <= 32768) is within 1 of r, which the two
+// exact checks correct.
 __device__ __forceinline__ uint32_t rms_exact(double S, double n, float inv_n) {
-    int32_t r = (int32_t)__fsqrt_rn((float)S * inv_n);
+    int32_t r = (int32_t)__builtin_amdgcn_sqrtf((float)S * inv_n);
     double rd = (double)r;
     r -= (n * rd * rd > S) ? 1 : 0;
     rd = (double)(r + 1);
@@ -151,7 +158,7 @@ __global__ void __launch_bounds__(256, MM_RMS_MINB) comp_rms_kernel(CompArgs a) 
     const int nd = (int)(d_first - (int64_t)gd * T);
     const int ch = a.ch;
     double n = (double)((f0 - lo0) * ch);
-    float inv = n > 0.0 ? 1.0f / (float)n : 0.f;
+    float inv = n > 0.0 ? __builtin_amdgcn_rcpf((float)n) : 0.f;  // (an estimate's factor only)
     const uint32_t r0 = a.r0[b];
     const double *lut = a.lut[b];
     const double Rf = a.release_frames[b], rR = a.rcp_release[b];
@@ -173,17 +180,23 @@ __global__ void __launch_bounds__(256, MM_RMS_MINB) comp_rms_kernel(CompArgs a) 
         p.drop = x[(uint32_t)k * G + gd + (uint32_t)wrap];
         return p;
     };
-    auto rms_step = [&](Pair p) {
+    // st: BoolTag<true> when no lane of the wave is in a chunk's first `look` frames
+    // (every wave but the few holding a chunk's first tiles): the window slides, n is fixed
+    auto rms_step = [&](Pair p, auto st) __attribute__((always_inline)) {
         const uint32_t r = rms_exact(S, n, inv);
         active += r >= r0 ? 1 : 0;
         rmx = max(rmx, r);
-        const bool drops = i_proc >= skip;
-        S += (double)frame_energy(p.in) - (drops ? (double)frame_energy(p.drop) : 0.0);
-        if (!drops) {  // window still growing (first `look` frames of a chunk only)
-            n += ch;
-            inv = 1.0f / (float)n;
+        if constexpr (decltype(st)::value) {
+            S += (double)frame_energy(p.in) - (double)frame_energy(p.drop);
+        } else {
+            const bool drops = i_proc >= skip;
+            S += (double)frame_energy(p.in) - (drops ? (double)frame_energy(p.drop) : 0.0);
+            if (!drops) {  // window still growing (first `look` frames of a chunk only)
+                n += ch;
+                inv = __builtin_amdgcn_rcpf((float)n);
+            }
+            ++i_proc;
         }
-        ++i_proc;
         return r;
     };
     // blocks of RMS_B frames: loads MM_RMS_NB blocks ahead; the block's M gathers
@@ -210,7 +223,7 @@ __global__ void __launch_bounds__(256, MM_RMS_MINB) comp_rms_kernel(CompArgs a) 
             }
         e += (uint32_t)pn * GS32;
     };
-    if (len > 0) {
+    auto run = [&](auto st) __attribute__((always_inline)) {
 #pragma unroll
         for (int k = 0; k < NB; ++k) {
 #pragma unroll
@@ -222,7 +235,7 @@ __global__ void __launch_bounds__(256, MM_RMS_MINB) comp_rms_kernel(CompArgs a) 
         auto block = [&](int k, int q, int nv) __attribute__((always_inline)) {
             uint32_t r[B];
 #pragma unroll
-            for (int j = 0; j < B; ++j) r[j] = j < nv ? rms_step(buf[k][j]) : 0u;
+            for (int j = 0; j < B; ++j) r[j] = j < nv ? rms_step(buf[k][j], st) : 0u;
             double m[B];
 #ifdef MM_RMS_NOGATHER  // timing experiment only (wrong M)
 #pragma unroll
@@ -255,6 +268,10 @@ __global__ void __launch_bounds__(256, MM_RMS_MINB) comp_rms_kernel(CompArgs a) 
                 if (k == nfull % NB) block(k, nfull, ntail);
         }
         flush(false);
+    };
+    if (len > 0) {
+        if (__all(skip == 0)) run(BoolTag<true>{});
+        else run(BoolTag<false>{});
     }
     // rows past the tile's frames (a partial last tile, the padding to TP): M = 0
     // (identity steps)
