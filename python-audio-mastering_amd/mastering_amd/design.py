@@ -28,6 +28,7 @@ MAX_DIM = 8
 CHUNK_MS = 30 * 1000  # AME:48
 DEFAULT_TILE = 225     # divides 30 s chunks at 11.025/22.05/44.1/48/88.2/96/192 kHz (round 4: T 75-250 swept,
                        # 225 fastest on C2, P_HOT, C3 and C5)
+NOCOMP_TILE = 125      # tile of jobs without the multiband compressor (EQ / K-weighting lanes)
 OPS_TILE = 125         # tile of the per-stage operators' look-back tables (== OPS_TILE in csrc/ops.hip)
 
 EQ_KEYS = ("bass_boost", "mid_cut", "presence_boost", "treble_boost")

@@ -72,7 +72,9 @@ class Job:
             bounds = design.chunk_bounds(self.frames_in, self.rate)
             nominal = design.pydub_frame(design.CHUNK_MS, self.rate)
             design.check_chunk_geometry(bounds, nominal, self.rate, multiband)
-            self.tile = design.choose_tile(nominal)
+            # without the compressor the chain is the IIR stages alone, which want the
+            # lanes of shorter tiles on a short track (C1: 0.139 ms at 125 against 0.188 at 225)
+            self.tile = design.choose_tile(nominal, None if multiband else design.NOCOMP_TILE)
             self.tiles_per_chunk = nominal // self.tile
         self.chunks = bounds
         self.frames_proc = bounds[-1][1] if bounds else 0
