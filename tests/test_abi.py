@@ -110,3 +110,25 @@ def test_solve_geometry_up_to_2_31_frames(rate):
         if prev is not None:  # per-chunk geometry does not depend on the length
             assert (g.tps, g.rows, g.cols_per_chunk, g.chunk_plane_bytes) == prev
         prev = (g.tps, g.rows, g.cols_per_chunk, g.chunk_plane_bytes)
+
+
+@pytest.mark.parametrize("rate", [11025, 16000, 22050, 32000, 44056, 44100, 48000, 88200, 96000, 192000])
+def test_tile_geometry_every_rate(rate):
+    """Tiles divide the 30 s chunk at every supported rate (225 frames where it divides,
+    else the nearest divisor counting the 25-row walk-block padding; 125 without the
+    compressor), and a super-tile is 4 tiles: the count the super-tile release records
+    assume (SJ_TPS in csrc/compressor.hip), so super jumps run at every rate."""
+    from mastering_amd import design, engine
+    chunk = design.pydub_frame(design.CHUNK_MS, rate)
+    t = design.choose_tile(chunk)
+    assert chunk % t == 0 and 64 <= t <= 512
+    if chunk % design.DEFAULT_TILE == 0:
+        assert t == design.DEFAULT_TILE
+    else:  # the fallback stays near the preferred length and wastes < 10 % of the walk rows
+        assert abs(t - design.DEFAULT_TILE) <= 40 and ((t + 24) // 25 * 25 - t) / t < 0.1
+    assert engine.comp_super_frames(rate, t) == 4 * t
+    tn = design.choose_tile(chunk, design.NOCOMP_TILE)
+    assert chunk % tn == 0
+    job_mb = engine.Job(chunk, rate, 2, {"multiband": True})
+    job_eq = engine.Job(chunk, rate, 2, {"multiband": False, "lufs": -14.0})
+    assert job_mb.tile == t and job_eq.tile == tn
