@@ -113,8 +113,7 @@ def intermediate_bytes(kernel, n, g, active, walked_per_launch):
         "pre_pointwise": 8 * n + 4 * n,
         "xover": 4 * n + 12 * n,              # q1 in; three int16-pair bands out
         "comp_rms": 12 * n + 24 * n,          # bands in; f64 M of every band-frame out (the M plane)
-        "comp_links": g * 3 * 8,              # active counts in; ranks out
-        "comp_describe": 8 * active,          # M of every active band-frame (release-jump records out: 64 B per active tile)
+        "comp_describe": 8 * active,          # M of every active band-frame (links + release-jump records: 128 B per active tile)
         "comp_pass0": 8 * active,             # M of every active band-frame
         "comp_fix": 8 * walked_per_launch,    # M of the re-walked frames
         "comp_apply": 8 * active + 12 * n + 4 * n,  # M of the active frames, bands in; mix out
