@@ -207,6 +207,16 @@ int mm_kweight_range_end(mm_ctx *ctx, double *end_state_host);
 /* Per-segment K-weighted energies given a carry-in state (host [dim] or NULL);
  * writes n_segs doubles to host. */
 int mm_hop_energies(mm_ctx *ctx, const double *carry_in_host, double *seg_energy_host);
+/* Device-resident variant of mm_hop_energies + all-reduce + gating + mm_finalize
+ * (VERDICT r03 item 7): writes this rank's n_segs energies at seg_offset of a zeroed
+ * device vector of n_global_segs, sums it over the communicator's ranks in place
+ * (RCCL, when mm_comm_init ran with nranks > 1), gates the whole track on the device
+ * (block b: segments [blk_s0[b], blk_s1[b]), energies scaled by block_scale), applies
+ * the gain towards `target` LUFS with the limiter and writes this rank's output to
+ * d_out; returns the whole track's loudness via *loudness. */
+int mm_shard_loudness_device(mm_ctx *ctx, const double *carry_in_host, int64_t n_global_segs, int64_t seg_offset,
+                             int64_t n_blocks, const int32_t *blk_s0_host, const int32_t *blk_s1_host,
+                             double block_scale, double target, void *d_out, double *loudness);
 /* Gated loudness from full-track segment energies (host, C restatement of
  * pyloudnorm's gating); returns L via *loudness. */
 int mm_gate_loudness(const mm_job *job, const double *seg_energy, double *loudness);

@@ -1585,6 +1585,62 @@ int mm_hop_energies(mm_ctx *c, const double *carry_in_host, double *seg_energy_h
     return kweight_energies(c, carry_in_host, seg_energy_host, nullptr);
 }
 
+// Time-sharded loudness without a host round trip for the energies (VERDICT r03
+// item 7): this rank's per-segment K-weighted energies go straight into a zeroed
+// device vector of the whole track's segments at seg_offset (a rank's segments are
+// consecutive global segments), ONE RCCL sum all-reduce runs in place on the
+// context's stream (when a communicator is set up), the whole track's gating runs
+// on the device (gate_kernel over the given block -> segment ranges), and finalize
+// reads the gain from device memory.  One host synchronisation before (the
+// envelope solve's convergence check, as mm_hop_energies) and one after (L).
+int mm_shard_loudness_device(mm_ctx *c, const double *carry_in_host, int64_t n_global_segs, int64_t seg_offset,
+                             int64_t n_blocks, const int32_t *blk_s0_host, const int32_t *blk_s1_host,
+                             double block_scale, double target, void *d_out, double *loudness_host) {
+    if (!c || !c->staged) return set_err(c, MM_ERR_STATE, "no staged job");
+    const int64_t nl = c->job.n_segs;
+    if (n_global_segs < 1 || seg_offset < 0 || seg_offset + nl > n_global_segs || n_blocks < 1 || !blk_s0_host ||
+        !blk_s1_host || !loudness_host)
+        return set_err(c, MM_ERR_ARG, "shard loudness: bad segment or block geometry");
+    for (int64_t b = 0; b < n_blocks; ++b)
+        if (blk_s0_host[b] < 0 || blk_s1_host[b] < blk_s0_host[b] || blk_s1_host[b] > n_global_segs)
+            return set_err(c, MM_ERR_ARG, "shard loudness: block %lld has segments [%d, %d) outside [0, %lld)",
+                           (long long)b, blk_s0_host[b], blk_s1_host[b], (long long)n_global_segs);
+    double *full, *gout;
+    int32_t *s0, *s1;
+    RET(get_buf(c, "shard_seg", (size_t)n_global_segs, &full));
+    RET(get_buf(c, "shard_gate", 2, &gout));
+    RET(get_buf(c, "shard_blk0", (size_t)n_blocks, &s0));
+    RET(get_buf(c, "shard_blk1", (size_t)n_blocks, &s1));
+    HIPCHK(c, hipMemsetAsync(full, 0, (size_t)n_global_segs * sizeof(double), c->stream));
+    if (c->G > 0 && nl > 0) {
+        double *seg;
+        RET(kweight_launch(c, carry_in_host, nullptr, &seg));
+        HIPCHK(c, hipMemcpyAsync(full + seg_offset, seg, (size_t)nl * sizeof(double), hipMemcpyDeviceToDevice,
+                                 c->stream));
+    }
+    bool conv;
+    RET(chain_check(c, &conv));
+    if (c->comm && c->nranks > 1) {
+        ncclResult_t r = ncclAllReduce(full, full, (size_t)n_global_segs, ncclDouble, ncclSum, c->comm, c->stream);
+        if (r != ncclSuccess) return set_err(c, MM_ERR_RCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
+    }
+    HIPCHK(c, hipMemcpyAsync(s0, blk_s0_host, (size_t)n_blocks * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(s1, blk_s1_host, (size_t)n_blocks * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+    GateArgs ga{};
+    ga.n_blocks = n_blocks;
+    ga.blk_s0 = s0;
+    ga.blk_s1 = s1;
+    ga.seg = full;
+    ga.scale = block_scale;
+    ga.target = target;
+    ga.out = gout;
+    RET(launch(c, "gate", gate_kernel, dim3(1), dim3(GATE_THREADS), 0, ga));
+    RET(finalize(c, 1.0, gout + 1, 1, d_out));
+    HIPCHK(c, hipMemcpyAsync(loudness_host, gout, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return MM_OK;
+}
+
 int mm_finalize(mm_ctx *c, double gain_linear, int use_gain, void *d_out) {
     if (!c || !c->staged) return set_err(c, MM_ERR_STATE, "no staged job");
     return finalize(c, gain_linear, nullptr, use_gain, d_out);

@@ -121,6 +121,15 @@ def compose_carry(z_all: np.ndarray, len_all, rate: int, rank: int) -> np.ndarra
     return s
 
 
+def block_segments(plan: RankPlan):
+    """Every loudness block's whole-track segment range [s0, s1) (int32), as
+    gate_loudness derives it."""
+    n = len(plan.seg_bounds) - 1
+    s0 = np.minimum(np.searchsorted(plan.seg_bounds, plan.block_lo), n).astype(np.int32)
+    s1 = np.minimum(np.searchsorted(plan.seg_bounds, plan.block_hi), n).astype(np.int32)
+    return s0, s1
+
+
 def gate_loudness(seg_energy: np.ndarray, plan: RankPlan) -> float:
     """pyloudnorm 0.1.1 integrated_loudness gating on whole-track segment energies
     (same restatement as mm_gate_loudness in csrc/mastering.hip)."""
@@ -206,6 +215,17 @@ class LibraryCollectives:
         return v
 
 
+class TorchLikeHost:
+    """world == 1 through the host orchestration (energies to the host, numpy gating):
+    the reference for the device-resident path in the tests."""
+
+    def all_gather(self, vec):
+        return np.asarray(vec, dtype=np.float64)[None, :]
+
+    def all_reduce_sum(self, vec):
+        return np.asarray(vec, dtype=np.float64)
+
+
 class LocalCollectives:
     """world == 1 (no communication)."""
 
@@ -249,6 +269,22 @@ class GpuBackend:
                                                     e.ctypes.data_as(native.c_double_p)), "mm_hop_energies")
         return e
 
+    def shard_loudness_device(self, carry: np.ndarray, plan: "RankPlan", target: float, d_out: int) -> float:
+        """Steps 3-5 with the energy vector kept in HBM (mm_shard_loudness_device): this
+        rank's segment energies into the whole-track vector, the RCCL sum all-reduce
+        in place (the context's communicator), device gating and the device gain into
+        mm_finalize.  Returns the whole track's loudness."""
+        c = np.ascontiguousarray(carry, dtype=np.float64)
+        n_glob = len(plan.seg_bounds) - 1
+        s0, s1 = block_segments(plan)
+        L = ctypes.c_double(0.0)
+        self.ctx.check(self.ctx.lib.mm_shard_loudness_device(
+            self.ctx.ptr, c.ctypes.data_as(native.c_double_p), n_glob, int(plan.local_to_global[0]), len(s0),
+            s0.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), s1.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+            float(plan.block_scale), float(target), ctypes.c_void_p(d_out), ctypes.byref(L)),
+            "mm_shard_loudness_device")
+        return float(L.value)
+
     def finalize(self, gain: float, use_gain: bool, d_out: int):
         self.ctx.check(self.ctx.lib.mm_finalize(self.ctx.ptr, float(gain), int(use_gain), ctypes.c_void_p(d_out)),
                        "mm_finalize")
@@ -267,6 +303,15 @@ def master_time_sharded(backend, plan: RankPlan, params: dict, d_in, d_out, coll
         z = backend.kweight_range_end()
         zl = coll.all_gather(np.concatenate([z, [float(plan.frames)]]))
         carry = compose_carry(zl[:, :4], zl[:, 4].astype(np.int64), plan.rate, plan.rank)
+        l2g = plan.local_to_global
+        if (isinstance(coll, (LibraryCollectives, LocalCollectives)) and hasattr(backend, "shard_loudness_device")
+                and len(l2g) and np.all(np.diff(l2g) == 1)):
+            # the library's own communicator (or none): energies, all-reduce, gating and
+            # gain stay on the device (a rank's segments are consecutive global ones)
+            L = backend.shard_loudness_device(carry, plan, float(lufs), d_out)
+            gain = 10.0 ** ((float(lufs) - L) / 20.0)
+            return {"loudness": L, "gain_linear": gain, "frames": plan.frames, "f0": plan.f0, "f1": plan.f1,
+                    "device_gate": True}
         local = backend.hop_energies(carry)
         full = np.zeros(len(plan.seg_bounds) - 1)
         np.add.at(full, plan.local_to_global, local)

@@ -77,7 +77,8 @@ class MMWavInfo(ctypes.Structure):
 # every symbol include/mastering.h declares (checked by tests/test_abi.py)
 EXPORTS = ("mm_create", "mm_destroy", "mm_last_error", "mm_sync", "mm_version", "mm_source_sha", "mm_master",
            "mm_master_device",
-           "mm_stage_chunks", "mm_kweight_range_end", "mm_hop_energies", "mm_gate_loudness", "mm_finalize",
+           "mm_stage_chunks", "mm_kweight_range_end", "mm_hop_energies", "mm_shard_loudness_device",
+           "mm_gate_loudness", "mm_finalize",
            "mm_read_mix", "mm_timing", "mm_kernel_stats", "mm_comm_unique_id", "mm_comm_init", "mm_comm_destroy",
            "mm_allreduce_sum_f64", "mm_allgather_f64", "mm_wav_probe", "mm_master_wav",
            "mm_op_pcm_to_float", "mm_op_saturation", "mm_op_stereo_width", "mm_op_quantize", "mm_op_soft_limiter",
@@ -119,6 +120,9 @@ def load():
             "mm_master_wav": ([vp, P(MMJob), ctypes.c_char_p, ctypes.c_char_p, P(MMResult)], ctypes.c_int),
             "mm_kweight_range_end": ([vp, c_double_p], ctypes.c_int),
             "mm_hop_energies": ([vp, c_double_p, c_double_p], ctypes.c_int),
+            "mm_shard_loudness_device": ([vp, c_double_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                          ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
+                                          ctypes.c_double, ctypes.c_double, vp, c_double_p], ctypes.c_int),
             "mm_gate_loudness": ([P(MMJob), c_double_p, c_double_p], ctypes.c_int),
             "mm_finalize": ([vp, ctypes.c_double, ctypes.c_int, vp], ctypes.c_int),
             "mm_read_mix": ([vp, P(ctypes.c_int16)], ctypes.c_int),
