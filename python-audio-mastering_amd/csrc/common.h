@@ -19,7 +19,9 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 
 // The value held by the partner lane (lane ^ 1) of a stereo lane pair: a DPP
 // quad_perm [1,0,3,2] move (VALU), not __shfl_xor's ds_bpermute LDS round trip.
-__device__ __forceinline__ int32_t pair_swap(int32_t v) { return __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false); }
+// (every lane reads a lane of its own quad, so no "old" value is ever kept:
+// mov_dpp with bound_ctrl needs no zero-initialised destination)
+__device__ __forceinline__ int32_t pair_swap(int32_t v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true); }
 __device__ __forceinline__ double pair_swap(double v) {
     const int64_t b = __double_as_longlong(v);
     const int32_t lo = pair_swap((int32_t)(b & 0xffffffff)), hi = pair_swap((int32_t)(b >> 32));

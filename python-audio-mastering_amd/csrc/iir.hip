@@ -22,12 +22,34 @@ namespace mm {
 
 // float_array_to_audio_segment (AME:123-126): clip to [-1,1] (NaN propagates),
 // * 32768, astype(int16) == trunc to int32 then wrap to 16 bits; NaN -> 0.
-__device__ __forceinline__ int16_t quantize(double v) {
-    if (v != v) return 0;
-    v = v > 1.0 ? 1.0 : v;
-    v = v < -1.0 ? -1.0 : v;
-    int32_t i = (int32_t)(v * 32768.0);
-    return (int16_t)i;
+// Three instructions: v * 2^15 is exact, v_cvt_i32_f64 truncates, saturates out
+// of range values (infinities included) and maps NaN to 0, and v_med3_i32 clamps
+// to [-32768, 32768] — the same integer as trunc(clip(v) * 32768) for every v.
+// The caller keeps the low 16 bits (32768 wraps to -32768, as astype(int16)).
+__device__ __forceinline__ int32_t quantize_i32(double v) {
+    int32_t i;
+    asm("v_cvt_i32_f64 %0, %1" : "=v"(i) : "v"(v * 32768.0));
+    return min(max(i, -32768), 32768);
+}
+__device__ __forceinline__ int16_t quantize(double v) { return (int16_t)quantize_i32(v); }
+
+// tanhf without a branch: OCML's __ocml_tanh_f32 (ROCm 7.2 ocml.bc) operation for
+// operation — |x| < 0.625: the odd polynomial |x| + x^2 |x| P(x^2) (FMAs), else
+// 1 - 2 / (exp(2|x|) + 1) with OCML's expf and v_rcp_f32 — both evaluated and one
+// selected, then copysign.  Bit-identical to tanhf (whose divergent if/else runs
+// both paths in most waves anyway, behind exec-mask branches that keep the
+// scheduler from overlapping a frame's tanh with the previous frame's f64 chain).
+__device__ __forceinline__ float tanh_sel(float x) {
+    const float ax = fabsf(x);
+    const float x2 = __fmul_rn(x, x);
+    float p = fmaf(x2, -0x1.758e7ap-8f, 0x1.521192p-6f);
+    p = fmaf(x2, p, -0x1.b8389cp-5f);
+    p = fmaf(x2, p, 0x1.110704p-3f);
+    p = fmaf(x2, p, -0x1.555532p-2f);
+    const float small = fmaf(x2, __fmul_rn(ax, p), ax);
+    const float e = expf(__fmul_rn(ax, 2.0f));
+    const float big = fmaf(-2.0f, __builtin_amdgcn_rcpf(__fadd_rn(e, 1.0f)), 1.0f);
+    return copysignf(ax < 0.625f ? small : big, x);
 }
 
 // apply_saturation (AME:128-134), f32 throughout; no FMA contraction so the
@@ -35,10 +57,23 @@ __device__ __forceinline__ int16_t quantize(double v) {
 __device__ __forceinline__ float saturate(float x, const SatArgs &s) {
 #ifdef MM_ABLATE_TANH  // timing-only builds (tools/ablate.sh): the exciter without its tanh
     float t = __fmul_rn(x, s.drive);
+#elif defined(MM_TANH_SEL)
+    float t = tanh_sel(__fmul_rn(x, s.drive));
 #else
     float t = tanhf(__fmul_rn(x, s.drive));
 #endif
     return __fadd_rn(__fmul_rn(s.keep, x), __fmul_rn(s.mix, t));
+}
+
+// apply_stereo_width (AME:136-144) on a lane pair, one formula for both lanes:
+// with y this lane's sample and o its partner's, the left lane's mid + side and
+// the right lane's mid - side are both RN(RN(y + o)/2 + RN(RN(y - o) * (w/2)))
+// (RN(o - y) = -RN(y - o); halving and w/2 are exact), and RN(s/2 + side) is
+// fma(s, 0.5, side).  No lane-dependent selects.  hw = width / 2.
+__device__ __forceinline__ double widen_pair(double y, double hw) {
+    const double o = pair_swap(y);
+    const double side = (y - o) * hw;
+    return fma(y + o, 0.5, side);
 }
 
 // DF2T section (scipy sosfilt / lfilter form): y = b0 x + z0;
@@ -79,6 +114,16 @@ __device__ __forceinline__ double df2t(double x, double &z0, double &z1, const d
 #ifndef MM_KW_NB
 #define MM_KW_NB 3
 #endif
+#ifndef MM_P1_UNROLL
+#define MM_P1_UNROLL 4
+#endif
+#ifndef MM_P1_DOT
+#define MM_P1_DOT 0
+#endif
+// pass 1 of the full-tile paths as the dot product with the zero-state response
+// (lookback.h resp_row) instead of the cascade
+constexpr bool P1_DOT = MM_P1_DOT != 0;
+constexpr int P1_UNROLL = MM_P1_UNROLL;
 constexpr int EQ_STAGE = MM_EQ_STAGE;  // frames per tile staged through LDS per step
 
 struct EqArgs {
@@ -170,20 +215,12 @@ __device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, doub
             if (n >= len) break;
             float x = row[j * CH + c];
             if (a.sat.on) x = saturate(x, a.sat);
-#ifndef MM_EQ_RECOMPUTE
             if (!P2) a.xs[((int64_t)n * a.G + g0 + t) * CH + c] = x;  // pass 2 reads it back coalesced
-#endif
             double y = (double)x;
 #pragma unroll
             for (int s = 0; s < NS; ++s) y = df2t<P2>(y, z[s][0], z[s][1], sos[s]);
             if (P2) {
-                if (CH == 2 && a.width_on) {  // apply_stereo_width (AME:136-144), f64
-                    const double o = pair_swap(y);
-                    const double yl = c == 0 ? y : o, yr = c == 0 ? o : y;
-                    const double mid = (yl + yr) / 2;
-                    const double side = (yl - yr) / 2 * a.width;
-                    y = c == 0 ? mid + side : mid - side;
-                }
+                if (CH == 2 && a.width_on) y = widen_pair(y, a.width * 0.5);  // AME:136-144, f64
                 const int64_t o = ((int64_t)n * a.G + g) * 2;
                 if (CH == 2) a.q_out[o + c] = quantize(y);
                 else *reinterpret_cast<short2 *>(a.q_out + o) = make_short2(quantize(y), 0);  // mono: R = 0
@@ -209,16 +246,129 @@ __device__ void eq_pass2(const EqArgs &a, int64_t g, int c, int len, double (&z)
             double y = (double)x;
 #pragma unroll
             for (int s = 0; s < NS; ++s) y = df2t<true>(y, z[s][0], z[s][1], sos[s]);
-            if (CH == 2 && a.width_on) {  // apply_stereo_width (AME:136-144), f64
-                const double o = pair_swap(y);
-                const double yl = c == 0 ? y : o, yr = c == 0 ? o : y;
-                const double mid = (yl + yr) / 2;
-                const double side = (yl - yr) / 2 * a.width;
-                y = c == 0 ? mid + side : mid - side;
-            }
+            if (CH == 2 && a.width_on) y = widen_pair(y, a.width * 0.5);  // AME:136-144, f64
             const int64_t o = ((int64_t)n * G + g) * 2;
             if (CH == 2) a.q_out[o + c] = quantize(y);
             else *reinterpret_cast<short2 *>(a.q_out + o) = make_short2(quantize(y), 0);  // mono: R = 0
+            ++n;
+        });
+}
+
+// ---- full-tile fast paths ----------------------------------------------------
+// Every block but the track's last holds TPB whole tiles, so its lanes run the
+// same T frames: the frame index is wave-uniform, every row address is a scalar
+// row base plus the lane's constant offset (no per-frame 64-bit index math), the
+// loops carry no per-lane exit, and the exciter / width switches are template
+// arguments instead of per-frame tests.
+
+// pass 1 from the LDS-staged input: exciter -> the f32 scratch a.xs (tile-major,
+// read back by pass 2) -> the zero-state cascade (fused: it only feeds the carry)
+template <int NS, int CH, bool I16, bool SAT, bool DOT>
+__device__ void eq_pass1_full(const EqArgs &a, const double *resp, int64_t g0, int t, int c, double (&z)[NS][2],
+                              float *stage) {
+    constexpr int TPB = LB_THREADS / CH;
+    constexpr int ROW = (EQ_STAGE + 1) * CH;
+    constexpr int ITEMS = TPB * EQ_STAGE / LB_THREADS;
+    const int T = a.T;
+    const int nsteps = (T + EQ_STAGE - 1) / EQ_STAGE;
+    const uint32_t tid = threadIdx.x;  // (unsigned: scalar row base + 32-bit lane offset)
+    const double(*sos)[5] = a.sos;
+    const int64_t GC = a.G * CH;          // floats per scratch row
+    float *xs0 = a.xs + g0 * CH;          // the block's first element of row 0 (uniform)
+    float regs[ITEMS][CH];
+    auto load = [&](int step) {
+#pragma unroll
+        for (int r = 0; r < ITEMS; ++r) {
+            const int idx = tid + r * LB_THREADS;
+            const int tt = idx / EQ_STAGE, j = idx % EQ_STAGE;
+            const int n = step * EQ_STAGE + j;
+            const int64_t f = (g0 + tt) * T + n;
+            const bool ok = n < T && f < a.N_in;
+            const int64_t fc = ok ? f : 0;
+            if constexpr (I16) {
+                if constexpr (CH == 2) {
+                    const short2 v = *reinterpret_cast<const short2 *>(a.in16 + 2 * fc);
+                    regs[r][0] = ok ? (float)v.x * (1.0f / 32768.0f) : 0.f;
+                    regs[r][1] = ok ? (float)v.y * (1.0f / 32768.0f) : 0.f;
+                } else {
+                    regs[r][0] = ok ? (float)a.in16[fc] * (1.0f / 32768.0f) : 0.f;
+                }
+            } else if constexpr (CH == 2) {
+                const float2 v = *reinterpret_cast<const float2 *>(a.in + 2 * fc);
+                regs[r][0] = ok ? v.x : 0.f;
+                regs[r][1] = ok ? v.y : 0.f;
+            } else {
+                const float v = a.in[fc];
+                regs[r][0] = ok ? v : 0.f;
+            }
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int r = 0; r < ITEMS; ++r) {
+            const int idx = tid + r * LB_THREADS;
+            const int tt = idx / EQ_STAGE, j = idx % EQ_STAGE;
+            float *dst = stage + buf * TPB * ROW + tt * ROW + j * CH;
+#pragma unroll
+            for (int q = 0; q < CH; ++q) dst[q] = regs[r][q];
+        }
+    };
+    load(0);
+    store(0);
+    lds_barrier();
+    for (int step = 0; step < nsteps; ++step) {
+        const int cur = step & 1;
+        if (step + 1 < nsteps) load(step + 1);
+        const float *row = stage + cur * TPB * ROW + t * ROW + c;
+        const int nj = min(EQ_STAGE, T - step * EQ_STAGE);  // uniform
+        float *xr = xs0 + (int64_t)(step * EQ_STAGE) * GC;
+#pragma unroll P1_UNROLL
+        for (int j = 0; j < nj; ++j) {
+            float x = row[j * CH];
+            if constexpr (SAT) x = saturate(x, a.sat);
+            (xr + (int64_t)j * GC)[tid] = x;
+            if constexpr (DOT) {  // z += h[T-1-n] x_n: 2NS independent FMAs, no cascade chain
+                double h[2 * NS];
+                resp_row(resp, step * EQ_STAGE + j, h);
+                const double y = (double)x;
+#pragma unroll
+                for (int s = 0; s < NS; ++s) {
+                    z[s][0] = fma(h[2 * s], y, z[s][0]);
+                    z[s][1] = fma(h[2 * s + 1], y, z[s][1]);
+                }
+            } else {
+                double y = (double)x;
+#pragma unroll
+                for (int s = 0; s < NS; ++s) y = df2t<false>(y, z[s][0], z[s][1], sos[s]);
+            }
+        }
+        if (step + 1 < nsteps) store(cur ^ 1);
+        lds_barrier();
+    }
+}
+
+// pass 2 from the scratch: EQ (scipy order) -> width -> int16, all rows uniform
+template <int NS, int CH, bool WIDTH>
+__device__ void eq_pass2_full(const EqArgs &a, int64_t g0, double (&z)[NS][2]) {
+    const double(*sos)[5] = a.sos;
+    const int T = a.T;
+    const uint32_t tid = threadIdx.x;  // (unsigned: scalar row base + 32-bit lane offset)
+    const int64_t GC = a.G * CH;
+    const float *xs0 = a.xs + g0 * CH;
+    const double hw = a.width * 0.5;
+    int16_t *q0 = a.q_out + g0 * 2;  // the block's first pair of row 0
+    const int64_t G2 = a.G * 2;
+    int n = 0;
+    stream<8, MM_EQ_NB, float>(
+        T, [&](int i) { return (xs0 + (int64_t)min(i, T - 1) * GC)[tid]; },
+        [&](float x) {
+            double y = (double)x;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) y = df2t<true>(y, z[s][0], z[s][1], sos[s]);
+            if constexpr (CH == 2 && WIDTH) y = widen_pair(y, hw);
+            int16_t *qr = q0 + (int64_t)n * G2;
+            if constexpr (CH == 2) qr[tid] = quantize(y);
+            else reinterpret_cast<short2 *>(qr)[tid] = make_short2(quantize(y), 0);  // mono: R = 0
             ++n;
         });
 }
@@ -246,7 +396,18 @@ __global__ void __launch_bounds__(LB_THREADS, 4) eq_kernel(EqArgs a, LbArgs lb, 
     double zs[NS][2];
 #pragma unroll
     for (int s = 0; s < NS; ++s) zs[s][0] = zs[s][1] = 0.0;
-    eq_pass<NS, CH, false, I16>(a, g0, t, c, len, zs, stage);
+    // block-uniform: every tile of the block is whole (all blocks but the track's last)
+    const bool full = (g0 + TPB) * a.T <= a.N_proc && (!P1_DOT || lb.resp);
+#ifdef MM_EQ_P1_GENERIC  // (ablation builds)
+    if (false) {
+#else
+    if (full) {
+#endif
+        if (a.sat.on) eq_pass1_full<NS, CH, I16, true, P1_DOT>(a, lb.resp, g0, t, c, zs, stage);
+        else eq_pass1_full<NS, CH, I16, false, P1_DOT>(a, lb.resp, g0, t, c, zs, stage);
+    } else {
+        eq_pass<NS, CH, false, I16>(a, g0, t, c, len, zs, stage);
+    }
     double z[DIM], s[DIM], rst[DIM];
 #pragma unroll
     for (int s_ = 0; s_ < NS; ++s_) {
@@ -262,11 +423,16 @@ __global__ void __launch_bounds__(LB_THREADS, 4) eq_kernel(EqArgs a, LbArgs lb, 
         zs[s_][0] = s[2 * s_];
         zs[s_][1] = s[2 * s_ + 1];
     }
-#ifdef MM_EQ_RECOMPUTE  // pass 2 re-stages the input and recomputes the exciter (no scratch)
-    eq_pass<NS, CH, true, I16>(a, g0, t, c, len, zs, stage);
+#ifdef MM_EQ_P2_GENERIC  // (ablation builds)
+    if (false) {
 #else
-    if (valid) eq_pass2<NS, CH>(a, g, c, len, zs);
+    if (full) {
 #endif
+        if (CH == 2 && a.width_on) eq_pass2_full<NS, CH, true>(a, g0, zs);
+        else eq_pass2_full<NS, CH, false>(a, g0, zs);
+    } else if (valid) {
+        eq_pass2<NS, CH>(a, g, c, len, zs);
+    }
 }
 
 // No active EQ stage: the chain stays f32 (AME:152-162 returns the f32 input;
@@ -376,6 +542,79 @@ __device__ __forceinline__ void xo_pass(const XoArgs &a, int64_t g, int c, int l
     }
 }
 
+// Full-tile fast path (every block but the track's last): uniform rows, scalar
+// row bases, int16 -> f64 in two instructions (q * 2^-15 is exact, and equals
+// AME:199's f32 q / 32768 widened), and the band energies as exact 64-bit integer
+// multiply-adds (v_mad_i64_i32) of the pre-wrap quantiser output (+-32768 square
+// alike); the tail sums take the frames n >= tail_from through a select on the
+// uniform frame index.
+template <int CH, bool P2>
+__device__ __forceinline__ void xo_pass_full(const XoArgs &a, const double *resp, int64_t g0, int tid,
+                                             double (&z)[4][2]) {
+    const double(*sos)[5] = a.sos;
+    const int T = a.T;
+    const int64_t G2 = a.G * 2;
+    const int16_t *qin0 = a.q_in + g0 * 2;  // the block's first element of row 0
+    const uint32_t lo = CH == 2 ? (uint32_t)tid : 2u * tid;  // this lane's int16 within the row
+    int16_t *b0 = a.band[0] + g0 * 2, *b1 = a.band[1] + g0 * 2, *b2 = a.band[2] + g0 * 2;
+    int pn = 0;
+    // exact integer sums in doubles (< 2^53); the tail weight is 0 or 1 (uniform)
+    double Ed[3] = {0.0, 0.0, 0.0}, td[3] = {0.0, 0.0, 0.0};
+    stream<8, MM_XO_NB, int16_t>(
+        T, [&](int i) { return (qin0 + (int64_t)min(i, T - 1) * G2)[lo]; },
+        [&](int16_t q) {
+            const double x = (double)(int32_t)q * (1.0 / 32768.0);  // AME:199 int16 -> f32, exact
+            if (!P2 && P1_DOT) {  // z += h[T-1-n] x_n (lb_resp rows): 8 independent FMAs
+                double h[8];
+                resp_row(resp, pn, h);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    z[k][0] = fma(h[2 * k], x, z[k][0]);
+                    z[k][1] = fma(h[2 * k + 1], x, z[k][1]);
+                }
+                ++pn;
+                return;
+            }
+            double yl = df2t<P2>(x, z[0][0], z[0][1], sos[0]);
+            yl = df2t<P2>(yl, z[1][0], z[1][1], sos[1]);
+            double yh = df2t<P2>(x, z[2][0], z[2][1], sos[2]);
+            yh = df2t<P2>(yh, z[3][0], z[3][1], sos[3]);
+            if (P2) {
+                const double ym = (x - yl) - yh;  // AME:202
+                const int32_t qi[3] = {quantize_i32(yl), quantize_i32(ym), quantize_i32(yh)};
+                const int64_t ro = (int64_t)pn * G2;
+                int16_t *rows[3] = {b0 + ro, b1 + ro, b2 + ro};
+#pragma unroll
+                for (int b = 0; b < 3; ++b) {
+                    if constexpr (CH == 2) rows[b][lo] = (int16_t)qi[b];
+                    else reinterpret_cast<short2 *>(rows[b])[(uint32_t)tid] = make_short2((int16_t)qi[b], 0);
+                    const double e = (double)(uint32_t)(qi[b] * qi[b]);  // <= 2^30 (v_mul_i32_i24)
+                    Ed[b] += e;
+                    td[b] = fma(pn >= a.tail_from[b] ? 1.0 : 0.0, e, td[b]);
+                }
+            }
+            ++pn;
+        });
+    if (P2) {
+        if (CH == 2) {  // L^2 + R^2 sums of the lane pair
+#pragma unroll
+            for (int b = 0; b < 3; ++b) {
+                Ed[b] += pair_swap(Ed[b]);
+                td[b] += pair_swap(td[b]);
+            }
+        }
+        const int c = CH == 2 ? (tid & 1) : 0;
+        const int64_t g = g0 + tid / CH;
+        if (c == 0) {
+#pragma unroll
+            for (int b = 0; b < 3; ++b) {
+                a.E[b][g] = Ed[b];
+                a.tail[b][g] = td[b];
+            }
+        }
+    }
+}
+
 template <int CH>
 __global__ void __launch_bounds__(LB_THREADS, 4) xover_kernel(XoArgs a, LbArgs lb, int64_t line_tiles) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -389,7 +628,10 @@ __global__ void __launch_bounds__(LB_THREADS, 4) xover_kernel(XoArgs a, LbArgs l
     const bool valid = g < a.G;
     const int len = valid ? (int)min((int64_t)a.T, a.N_proc - g * a.T) : 0;
     double zs[4][2] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
-    if (valid) xo_pass<CH, false>(a, g, c, len, zs);
+    const int64_t g0 = (int64_t)blk * TPB;
+    const bool full = (g0 + TPB) * a.T <= a.N_proc && (!P1_DOT || lb.resp);  // block-uniform
+    if (full) xo_pass_full<CH, false>(a, lb.resp, g0, tid, zs);
+    else if (valid) xo_pass<CH, false>(a, g, c, len, zs);
     double z[8], s[8], rst[8];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -403,7 +645,8 @@ __global__ void __launch_bounds__(LB_THREADS, 4) xover_kernel(XoArgs a, LbArgs l
         zs[k][0] = s[2 * k];
         zs[k][1] = s[2 * k + 1];
     }
-    if (valid) xo_pass<CH, true>(a, g, c, len, zs);
+    if (full) xo_pass_full<CH, true>(a, lb.resp, g0, tid, zs);
+    else if (valid) xo_pass<CH, true>(a, g, c, len, zs);
 }
 
 // ----------------------------------------------------------- K-weighting stage
