@@ -62,7 +62,7 @@ import numpy as np  # noqa: E402
 METRIC = "stereo frames/sec through full mastering chain, 44.1 kHz f32; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 CHAIN_BYTES_PER_FRAME = 16  # f32 L,R in + f32 L,R out
-PROFILE_ROUND = "r04"  # profiles/<round>_<workload>_pmc_summary.json carry the PMC traffic
+PROFILE_ROUND = "r05"  # profiles/<round>_<workload>_pmc_summary.json carry the PMC traffic
 P_FULL = {"bass_boost": 4.0, "mid_cut": 3.0, "presence_boost": 1.0, "treble_boost": 3.0,
           "saturation": 30, "width": 1.3, "multiband": True, "lufs": -14.0}
 P_HOT = dict(P_FULL, low_thresh=-16.0, mid_thresh=-21.0, high_thresh=-27.0)
@@ -317,6 +317,30 @@ def valu_ceiling(prof, dom):
             "per_kernel_frac": {k: round(v["frac"], 4) for k, v in per.items()}}
 
 
+LANE_OPS_PEAK = 1024 * 16 * 2.4e9  # VALU lane-instructions/s: 1024 SIMDs x 16 lanes x 2.4 GHz (39.3 T)
+
+
+def valu_floor(prof, n_frames, ms_step):
+    """The chain's VALU floor: lane-instructions per stereo frame
+    (SQ_INSTS_VALU x 64 lanes x launches per step over the step's frames, per kernel
+    and summed) and the time the chip needs to issue them at one wave64 instruction
+    per SIMD every 4 cycles (39.3 T lane-instr/s), against ms_per_step."""
+    ks = prof.get("kernels", {})
+    per = {}
+    for k, q in ks.items():
+        n = (q.get("sq") or {}).get("SQ_INSTS_VALU")
+        if n:
+            per[k] = n * 64.0 * q.get("launches_per_step", 1.0) / n_frames
+    if not per:
+        return None
+    tot = sum(per.values())
+    floor_ms = tot * n_frames / LANE_OPS_PEAK * 1e3
+    return {"lane_instr_per_frame": tot, "floor_ms": floor_ms, "frac": floor_ms / ms_step,
+            "peak_lane_instr_per_s": LANE_OPS_PEAK,
+            "per_kernel_lane_instr_per_frame": {k: round(v, 1) for k, v in sorted(per.items(), key=lambda kv: -kv[1])},
+            "scope": "SQ_INSTS_VALU x 64 x launches per step / frames per step, summed over the chain's kernels"}
+
+
 def profile_summary(tag):
     path = os.path.join(ROOT, "profiles", f"{tag}_pmc_summary.json")
     try:
@@ -376,6 +400,13 @@ def main():
         run.step(want_results=(i == P - 1))
     stats = run.ctx.kernel_stats()
     run.ctx.timing(False)
+    if world > 1 and args.workload == "C4":
+        # every rank gated the same all-reduced vector: the same loudness and gain on
+        # every rank, checked before rank 0 reports
+        lg = [None] * world
+        dist.all_gather_object(lg, (run.results[0]["loudness"], run.results[0]["gain_linear"]))
+        if any(v != lg[0] for v in lg):
+            raise SystemExit(f"C4: ranks disagree on loudness / gain: {lg}")
 
     if rank == 0:
         from mastering_amd import native
@@ -409,7 +440,7 @@ def main():
         tag = args.profile_tag or f"{PROFILE_ROUND}_{args.workload}" + ("" if args.params == default_params else args.params)
         prof, prof_path = profile_summary(tag)
         traffic = limiter = dom_traffic = None
-        valu = None
+        valu = vfloor = None
         prof_note = f"no profile at {os.path.relpath(prof_path, ROOT)}"
         if prof is not None:
             if prof.get("source_sha") != sha:
@@ -422,6 +453,7 @@ def main():
                 k = prof.get("kernels", {}).get(dom, {})
                 dom_traffic = k.get("bytes_per_launch")
                 valu = valu_ceiling(prof, dom)
+                vfloor = valu_floor(prof, n_frames, ms_step)
         line = {
             "metric": METRIC, "value": value, "unit": "stereo frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
@@ -449,7 +481,7 @@ def main():
                                                                    if ibl is not None else None),
                                              "avg_launch_ms": avg_s * 1e3,
                                              "launches_per_step": launches, "traffic": dom_traffic},
-                         "valu_ceiling": valu},
+                         "valu_ceiling": valu, "valu": vfloor},
             "chain": {"device_ms_per_step": sum(v[0] for v in per.values()),
                       "comp_iters": iters, "comp_active_frames": active, "comp_rewalked_frames": walked, "comp_jumped_frames": jumped,
                       "kernels_ms_per_step": {k: round(v[0], 4) for k, v in per.items()}},

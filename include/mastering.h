@@ -138,7 +138,7 @@ typedef struct mm_solve_geom {
     int32_t tile_rows;       /* M-plane rows per tile: T rounded up to whole walk
                                 load blocks (extra rows hold M = 0)            */
     int32_t rows;            /* rows per column: tps * tile_rows + prefetch pad  */
-    int32_t _pad;
+    int32_t walk_block;      /* rows per walk load block (tile_rows is a multiple)  */
     int64_t cols_per_chunk;  /* super-tile columns per chunk (whole blocks of 64) */
     int64_t chunks;
     int64_t chunk_plane_bytes; /* one chunk's part of one band's M plane: walked
@@ -152,9 +152,11 @@ int mm_destroy(mm_ctx *ctx);
 const char *mm_last_error(mm_ctx *ctx);
 int mm_sync(mm_ctx *ctx);
 /* ABI version: 2 = mm_band.lut_key and mm_result.comp_jumped (round 3),
-   mm_solve_geometry (round 4).  A caller built against an older header must
+   mm_solve_geometry (round 4); 3 = mm_solve_geom.walk_block, the device loudness
+   path in composable steps with a world check and the applied gain returned,
+   device-pointer collectives (round 5).  A caller built against an older header must
    refuse a library whose version differs from its own MM_ABI_VERSION. */
-#define MM_ABI_VERSION 2
+#define MM_ABI_VERSION 3
 int mm_version(void);
 /* The envelope-solve geometry of a job (no context, no GPU).  MM_ERR_ARG if a
    chunk's plane would not fit 32-bit offsets (no track length below 2^31 frames
@@ -208,15 +210,25 @@ int mm_kweight_range_end(mm_ctx *ctx, double *end_state_host);
  * writes n_segs doubles to host. */
 int mm_hop_energies(mm_ctx *ctx, const double *carry_in_host, double *seg_energy_host);
 /* Device-resident variant of mm_hop_energies + all-reduce + gating + mm_finalize
- * (VERDICT r03 item 7): writes this rank's n_segs energies at seg_offset of a zeroed
- * device vector of n_global_segs, sums it over the communicator's ranks in place
- * (RCCL, when mm_comm_init ran with nranks > 1), gates the whole track on the device
- * (block b: segments [blk_s0[b], blk_s1[b]), energies scaled by block_scale), applies
- * the gain towards `target` LUFS with the limiter and writes this rank's output to
- * d_out; returns the whole track's loudness via *loudness. */
+ * (VERDICT r03 item 7), in three composable steps (the collective in between may be
+ * the library's communicator or torch.distributed over the same device buffer):
+ * mm_shard_energies_device zeroes the caller's device vector d_full[n_global_segs]
+ * and writes this rank's n_segs energies at seg_offset (synchronous on return);
+ * mm_gate_finalize_device gates the whole track on the device (block b: segments
+ * [blk_s0[b], blk_s1[b]), energies scaled by block_scale), applies the gain towards
+ * `target` LUFS with the limiter, writes this rank's output to d_out and returns
+ * {L, applied gain} in loudness_gain[2]. */
+int mm_shard_energies_device(mm_ctx *ctx, const double *carry_in_host, int64_t n_global_segs, int64_t seg_offset,
+                             double *d_full);
+int mm_gate_finalize_device(mm_ctx *ctx, const double *d_full, int64_t n_global_segs, int64_t n_blocks,
+                            const int32_t *blk_s0_host, const int32_t *blk_s1_host, double block_scale,
+                            double target, void *d_out, double *loudness_gain);
+/* All three with the library's communicator between them: `world` is the plan's rank
+ * count; world > 1 needs mm_comm_init over exactly `world` ranks on this context
+ * (MM_ERR_STATE otherwise: each rank would gate only its own part of the vector). */
 int mm_shard_loudness_device(mm_ctx *ctx, const double *carry_in_host, int64_t n_global_segs, int64_t seg_offset,
                              int64_t n_blocks, const int32_t *blk_s0_host, const int32_t *blk_s1_host,
-                             double block_scale, double target, void *d_out, double *loudness);
+                             double block_scale, double target, int32_t world, void *d_out, double *loudness_gain);
 /* Gated loudness from full-track segment energies (host, C restatement of
  * pyloudnorm's gating); returns L via *loudness. */
 int mm_gate_loudness(const mm_job *job, const double *seg_energy, double *loudness);
@@ -289,6 +301,10 @@ int mm_comm_destroy(mm_ctx *ctx);
 int mm_allreduce_sum_f64(mm_ctx *ctx, double *host_buf, int64_t n);
 /* All-gather of n doubles per rank: out = [nranks * n]. */
 int mm_allgather_f64(mm_ctx *ctx, const double *host_in, double *host_out, int64_t n);
+/* The same two collectives on device buffers of this context's device (no host
+ * staging; synchronous on return). */
+int mm_allreduce_sum_f64_device(mm_ctx *ctx, double *d_buf, int64_t n);
+int mm_allgather_f64_device(mm_ctx *ctx, const double *d_in, double *d_out, int64_t n);
 
 #ifdef __cplusplus
 }

@@ -124,6 +124,7 @@ __device__ __forceinline__ double *chunk_plane(const CompArgs &a, int b, int64_t
 #ifndef MM_RMS_MINB
 #define MM_RMS_MINB 1
 #endif
+#ifdef MM_RMS_V1  // round-4 lane mapping (A/B builds)
 __global__ void __launch_bounds__(256, MM_RMS_MINB) comp_rms_kernel(CompArgs a) {
     const int b = blockIdx.y;
     const int64_t wv = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -296,6 +297,209 @@ __global__ void __launch_bounds__(256, MM_RMS_MINB) comp_rms_kernel(CompArgs a) 
         atomicAdd(a.total[b] + c, active);
     }
 }
+#else
+// rms_exact with one correction: the f32 estimate of sqrt(S * (1/n)) taken with
+// the reciprocal scaled by (1 - 2^-18) (inv_b) lies in sqrt(S/n) * [1 - 2^-19 -
+// 2^-22, 1 - 2^-19 + 2^-22] (rcp, product and sqrt each within a few ulp), so
+// below sqrt(S/n) and above it minus 0.07 at r <= 32768: its truncation is r or
+// r - 1, and one exact check n (r+1)^2 <= S (integers below 2^53 in f64) fixes it.
+__device__ __forceinline__ uint32_t rms_exact1(double S, double n, float inv_b) {
+    int32_t r = (int32_t)__builtin_amdgcn_sqrtf((float)S * inv_b);
+    const double rd = (double)(r + 1);
+    r += (n * rd * rd <= S) ? 1 : 0;
+    return (uint32_t)r;
+}
+__device__ __forceinline__ float rcp_biased(double n) {
+    return __fmul_rn(__builtin_amdgcn_rcpf((float)n), 1.0f - 0x1p-18f);
+}
+// x^2 + y^2 of one frame in one v_dot2_i32_i16 (the 2^31 of two -32768s wraps to the
+// same uint32)
+__device__ __forceinline__ uint32_t frame_energy2(short2 v) {
+    uint32_t r;  // (VOP3P with an inline 0 accumulator: no v_mov to clear a v_dot2c destination)
+    asm("v_dot2_i32_i16 %0, %1, %1, 0" : "=v"(r) : "v"(v));
+    return r;
+}
+// max of two non-NaN doubles without fmax's operand canonicalisation
+__device__ __forceinline__ double vmax(double x, double y) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+    return r;
+}
+
+// Lanes of a wave take 64 CONSECUTIVE tiles (wave w of column block cb: tiles
+// 64 TPS cb + 64 w + lane of the chunk), so every band load is one 256-byte run and,
+// in the steady state (no lane in its chunk's first `look` frames, every tile
+// whole), the frame row of a load and of its drop frame is the same for all lanes:
+// a scalar row base plus the lane's tile.  M stores go to the super-tile-major
+// plane as before (four 128-byte runs per wave store: 16 columns at each of the
+// TPS = 4 tile positions).  The per-frame exact rms needs one correction
+// (rms_exact1); energies are single v_dot2 instructions.
+__global__ void __launch_bounds__(256, MM_RMS_MINB) comp_rms_kernel(CompArgs a) {
+    const int b = blockIdx.y;
+    const int64_t wv = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int64_t cbk = wv / a.TPS;                 // global column block
+    const int wq = (int)(wv - cbk * a.TPS);
+    const int64_t cc = (cbk * 64) / a.SPC;          // its chunk (SPC: whole column blocks)
+    const int64_t jt = (cbk * 64 - cc * a.SPC) * a.TPS + (int64_t)wq * 64 + lane;  // tile in the chunk
+    const int64_t g = cc * a.K + jt;
+    if (jt >= a.K || g >= a.G) return;  // past the chunk's tiles or the track
+    const int64_t sc = cc * a.SPC + jt / a.TPS;     // its column
+    const int kc = (int)(jt % a.TPS);
+    const short2 *x = a.band[b];
+    const int look = a.look[b];
+    const int T = a.T;
+    const uint32_t G = (uint32_t)a.G, g32 = (uint32_t)g;
+    const int64_t f0 = g * T;
+    const int64_t chunk0 = cc * a.K * T;
+    const int len = (int)min((int64_t)T, a.N_proc - f0);
+    const int64_t lo0 = max(chunk0, f0 - look);
+    double S = 0.0;
+    {
+        const int kf = look / T;
+        for (int t = 1; t <= kf; ++t)
+            if ((g - t) * T >= chunk0) S += a.E[b][g - t];
+        if (look % T != 0 && (g - kf - 1) * T >= chunk0) S += a.tail[b][g - kf - 1];
+    }
+    const int64_t d_first = max(f0 - look, chunk0);
+    const int skip = (int)(d_first - (f0 - look));
+    const uint32_t gd = (uint32_t)(d_first / T);
+    const int nd = (int)(d_first - (int64_t)gd * T);
+    const int ch = a.ch;
+    double n = (double)((f0 - lo0) * ch);
+    float inv = n > 0.0 ? rcp_biased(n) : 0.f;
+    const uint32_t r0 = a.r0[b];
+    const double *lut = a.lut[b];
+    const double Rf = a.release_frames[b], rR = a.rcp_release[b];
+    constexpr uint32_t GS32 = 64;
+    double *Mo = chunk_plane(a, b, cc);
+    uint32_t e = col_elem(a, sc) + (uint32_t)(kc * a.TP) * GS32;
+    int i_proc = 0, active = 0;
+    uint32_t rmx = 0;
+    struct Pair {
+        short2 in, drop;
+    };
+    // steady waves: uniform rows; the drop frame of frame i is row (nd + i) mod T of
+    // tile gd (+1 past the wrap), gd - g the same for every lane
+    const bool steady = __all(skip == 0 && len == T && look > 0);
+    // (uniform when steady: taken from the first lane so the row bases live in SGPRs)
+    const int64_t dgo = (int64_t)__builtin_amdgcn_readfirstlane((int)((int64_t)gd - g));
+    const int nd_u = __builtin_amdgcn_readfirstlane(nd);
+    auto ld_steady = [&](int i) {
+        i = min(i, T - 1);
+        Pair p;
+        p.in = (x + (int64_t)i * G)[g32];
+        int k = nd_u + i;
+        const int wrap = k >= T ? 1 : 0;
+        k -= wrap * T;
+        p.drop = (x + (int64_t)k * G + dgo + wrap)[g32];
+        return p;
+    };
+    auto ld = [&](int i) {
+        i = min(i, len - 1);
+        Pair p;
+        p.in = x[(uint32_t)i * G + g32];
+        int k = nd + max(i - skip, 0);
+        const int wrap = k >= T ? 1 : 0;
+        k -= wrap * T;
+        p.drop = x[(uint32_t)k * G + gd + (uint32_t)wrap];
+        return p;
+    };
+    auto rms_step = [&](Pair p, auto st) __attribute__((always_inline)) {
+        uint32_t r;
+        if constexpr (decltype(st)::value) {
+            r = rms_exact1(S, n, inv);
+            S += (double)frame_energy2(p.in) - (double)frame_energy2(p.drop);
+        } else {
+            r = n > 0.0 ? rms_exact1(S, n, inv) : 0u;
+            const bool drops = i_proc >= skip;
+            S += (double)frame_energy2(p.in) - (drops ? (double)frame_energy2(p.drop) : 0.0);
+            if (!drops) {  // window still growing (first `look` frames of a chunk only)
+                n += ch;
+                inv = rcp_biased(n);
+            }
+            ++i_proc;
+        }
+        active += r >= r0 ? 1 : 0;
+        rmx = max(rmx, r);
+        return r;
+    };
+    constexpr int B = RMS_B, NB = MM_RMS_NB;
+    Pair buf[NB][B];
+    double mq[B];
+    int pn = 0;
+    double ce = 0.0, De = 0.0;
+    auto flush = [&](bool whole) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < B; ++j)
+            if (whole || j < pn) {
+                Mo[e + (uint32_t)j * GS32] = mq[j];
+                const double d = div_cr(mq[j], Rf, rR);
+                ce = vmax(mq[j], ce - d);
+                De += d;
+            }
+        e += (uint32_t)pn * GS32;
+    };
+    auto run = [&](auto st, auto &&load, int L) __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+#pragma unroll
+            for (int j = 0; j < B; ++j) buf[k][j] = load(k * B + j);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        auto block = [&](int k, int q, int nv) __attribute__((always_inline)) {
+            uint32_t r[B];
+#pragma unroll
+            for (int j = 0; j < B; ++j) r[j] = j < nv ? rms_step(buf[k][j], st) : 0u;
+            double m[B];
+#pragma unroll
+            for (int j = 0; j < B; ++j) m[j] = lut[r[j]];
+            __builtin_amdgcn_sched_barrier(0);
+            if (q > 0) flush(true);
+#pragma unroll
+            for (int j = 0; j < B; ++j) buf[k][j] = load((q + NB) * B + j);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < B; ++j) mq[j] = m[j];
+            pn = nv;
+        };
+        const int nfull = L / B, ntail = L - nfull * B;
+        int q = 0;
+        for (; q + NB <= nfull; q += NB) {
+#pragma unroll
+            for (int k = 0; k < NB; ++k) block(k, q + k, B);
+        }
+#pragma unroll
+        for (int k = 0; k < NB; ++k)
+            if (q + k < nfull) block(k, q + k, B);
+        if (ntail) {
+#pragma unroll
+            for (int k = 0; k < NB; ++k)
+                if (k == nfull % NB) block(k, nfull, ntail);
+        }
+        flush(false);
+    };
+    if (steady) run(BoolTag<true>{}, ld_steady, T);
+    else if (len > 0) run(BoolTag<false>{}, ld, len);
+    for (int i = max(len, 0); i < a.TP; ++i, e += GS32) Mo[e] = 0.0;
+    a.cnt[b][g] = active;
+    a.mmax[b][g] = lut[rmx];
+    {  // active tiles of the column block (the wave's tiles share it)
+        const int na = (int)__popcll(__ballot(active != 0));
+        if (__lane_id() == __builtin_amdgcn_readfirstlane(__lane_id()) && na)
+            atomicAdd(a.cbtot[b] + (sc >> 6), na);
+    }
+    reinterpret_cast<double2 *>(a.ced[b])[g] = make_double2(ce, De);
+    const int c = (int)cc;
+    if (__ballot(1) == ~0ull) {
+        int v = active;
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if (__lane_id() == 0 && v) atomicAdd(a.total[b] + c, v);
+    } else if (active) {
+        atomicAdd(a.total[b] + c, active);
+    }
+}
+#endif
 
 
 struct BandStep {
@@ -1142,12 +1346,82 @@ __device__ __forceinline__ double neg_div20(double att) {
     return fma(rem, 0.05, q);
 }
 
+// 2^(j/64), j < 64, as double-double {hi, lo} (hi = RN(2^(j/64)), lo = RN(2^(j/64) - hi);
+// generated with Python's decimal module at 60 digits)
+__constant__ double2 EXP2_TAB64[64] = {
+    {0x1.0000000000000p+0, 0x0.0p+0}, {0x1.02c9a3e778061p+0, -0x1.19083535b085dp-56},
+    {0x1.059b0d3158574p+0, 0x1.d73e2a475b465p-55}, {0x1.0874518759bc8p+0, 0x1.186be4bb284ffp-57},
+    {0x1.0b5586cf9890fp+0, 0x1.8a62e4adc610bp-54}, {0x1.0e3ec32d3d1a2p+0, 0x1.03a1727c57b53p-59},
+    {0x1.11301d0125b51p+0, -0x1.6c51039449b3ap-54}, {0x1.1429aaea92de0p+0, -0x1.32fbf9af1369ep-54},
+    {0x1.172b83c7d517bp+0, -0x1.19041b9d78a76p-55}, {0x1.1a35beb6fcb75p+0, 0x1.e5b4c7b4968e4p-55},
+    {0x1.1d4873168b9aap+0, 0x1.e016e00a2643cp-54}, {0x1.2063b88628cd6p+0, 0x1.dc775814a8495p-55},
+    {0x1.2387a6e756238p+0, 0x1.9b07eb6c70573p-54}, {0x1.26b4565e27cddp+0, 0x1.2bd339940e9d9p-55},
+    {0x1.29e9df51fdee1p+0, 0x1.612e8afad1255p-55}, {0x1.2d285a6e4030bp+0, 0x1.0024754db41d5p-54},
+    {0x1.306fe0a31b715p+0, 0x1.6f46ad23182e4p-55}, {0x1.33c08b26416ffp+0, 0x1.32721843659a6p-54},
+    {0x1.371a7373aa9cbp+0, -0x1.63aeabf42eae2p-54}, {0x1.3a7db34e59ff7p+0, -0x1.5e436d661f5e3p-56},
+    {0x1.3dea64c123422p+0, 0x1.ada0911f09ebcp-55}, {0x1.4160a21f72e2ap+0, -0x1.ef3691c309278p-58},
+    {0x1.44e086061892dp+0, 0x1.89b7a04ef80d0p-59}, {0x1.486a2b5c13cd0p+0, 0x1.3c1a3b69062f0p-56},
+    {0x1.4bfdad5362a27p+0, 0x1.d4397afec42e2p-56}, {0x1.4f9b2769d2ca7p+0, -0x1.4b309d25957e3p-54},
+    {0x1.5342b569d4f82p+0, -0x1.07abe1db13cadp-55}, {0x1.56f4736b527dap+0, 0x1.9bb2c011d93adp-54},
+    {0x1.5ab07dd485429p+0, 0x1.6324c054647adp-54}, {0x1.5e76f15ad2148p+0, 0x1.ba6f93080e65ep-54},
+    {0x1.6247eb03a5585p+0, -0x1.383c17e40b497p-54}, {0x1.6623882552225p+0, -0x1.bb60987591c34p-54},
+    {0x1.6a09e667f3bcdp+0, -0x1.bdd3413b26456p-54}, {0x1.6dfb23c651a2fp+0, -0x1.bbe3a683c88abp-57},
+    {0x1.71f75e8ec5f74p+0, -0x1.16e4786887a99p-55}, {0x1.75feb564267c9p+0, -0x1.0245957316dd3p-54},
+    {0x1.7a11473eb0187p+0, -0x1.41577ee04992fp-55}, {0x1.7e2f336cf4e62p+0, 0x1.05d02ba15797ep-56},
+    {0x1.82589994cce13p+0, -0x1.d4c1dd41532d8p-54}, {0x1.868d99b4492edp+0, -0x1.fc6f89bd4f6bap-54},
+    {0x1.8ace5422aa0dbp+0, 0x1.6e9f156864b27p-54}, {0x1.8f1ae99157736p+0, 0x1.5cc13a2e3976cp-55},
+    {0x1.93737b0cdc5e5p+0, -0x1.75fc781b57ebcp-57}, {0x1.97d829fde4e50p+0, -0x1.d185b7c1b85d1p-54},
+    {0x1.9c49182a3f090p+0, 0x1.c7c46b071f2bep-56}, {0x1.a0c667b5de565p+0, -0x1.359495d1cd533p-54},
+    {0x1.a5503b23e255dp+0, -0x1.d2f6edb8d41e1p-54}, {0x1.a9e6b5579fdbfp+0, 0x1.0fac90ef7fd31p-54},
+    {0x1.ae89f995ad3adp+0, 0x1.7a1cd345dcc81p-54}, {0x1.b33a2b84f15fbp+0, -0x1.2805e3084d708p-57},
+    {0x1.b7f76f2fb5e47p+0, -0x1.5584f7e54ac3bp-56}, {0x1.bcc1e904bc1d2p+0, 0x1.23dd07a2d9e84p-55},
+    {0x1.c199bdd85529cp+0, 0x1.11065895048ddp-55}, {0x1.c67f12e57d14bp+0, 0x1.2884dff483cadp-54},
+    {0x1.cb720dcef9069p+0, 0x1.503cbd1e949dbp-56}, {0x1.d072d4a07897cp+0, -0x1.cbc3743797a9cp-54},
+    {0x1.d5818dcfba487p+0, 0x1.2ed02d75b3707p-55}, {0x1.da9e603db3285p+0, 0x1.c2300696db532p-54},
+    {0x1.dfc97337b9b5fp+0, -0x1.1a5cd4f184b5cp-54}, {0x1.e502ee78b3ff6p+0, 0x1.39e8980a9cc8fp-55},
+    {0x1.ea4afa2a490dap+0, -0x1.e9c23179c2893p-54}, {0x1.efa1bee615a27p+0, 0x1.dc7f486a4b6b0p-54},
+    {0x1.f50765b6e4540p+0, 0x1.9d3e12dd8a18bp-54}, {0x1.fa7c1819e90d8p+0, 0x1.74853f3a5931ep-55}};
+
+// 10^y for the compressor's gains (y = RN(-att/20) <= 0): 2^(y log2 10) with the
+// exponent split t = k/64 + r (|r| <= 1/128; y log2 10 carried to ~106 bits by two
+// FMAs), 2^r by its degree-6 Taylor polynomial (truncation 3e-20) and 2^(k/64) from
+// the double-double table in LDS.  Within 1.5 ulp of 10^y on [-3, 0] (pydub's libm
+// pow within 0.5): a gain one or two ulp off moves floor(x * gain) (audioop.mul) only
+// when x * gain lies within ~1e-11 of an integer, as with OCML's exp10.
+// y = 0 gives exactly 1.0 (the identity gain of an unattenuated frame).  18 VALU + one
+// LDS read against OCML exp10's ~70.
+__device__ __forceinline__ double exp10_tab(double y, const double2 *tab) {
+    constexpr double L_HI = 0x1.a934f0979a371p+1, L_LO = 0x1.7f2495fb7fa6dp-53;
+    const double th = y * L_HI;
+    const double tl = fma(y, L_LO, fma(y, L_HI, -th));
+    const double kd = rint(th * 64.0);
+    const int k = (int)kd;
+    const double r = fma(-kd, 0.015625, th) + tl;
+    double p = 0x1.430912f86c787p-13;
+    p = fma(p, r, 0x1.5d87fe78a6731p-10);
+    p = fma(p, r, 0x1.3b2ab6fba4e77p-7);
+    p = fma(p, r, 0x1.c6b08d704a0c0p-5);
+    p = fma(p, r, 0x1.ebfbdff82c58fp-3);
+    p = fma(p, r, 0x1.62e42fefa39efp-1);
+    p = fma(p, r, 1.0);
+    const double2 t = tab[k & 63];
+    return ldexp(fma(t.x, p, t.y * p), k >> 6);
+}
+
 #ifndef MM_APPLY_MINB
 #define MM_APPLY_MINB 1
+#endif
+#ifdef MM_APPLY_OCML  // (A/B builds: OCML's exp10)
+#define MM_GAIN(att) exp10(neg_div20(att))
+#else
+#define MM_GAIN(att) exp10_tab(neg_div20(att), etab)
 #endif
 __global__ void __launch_bounds__(192, MM_APPLY_MINB) comp_apply_kernel(CompArgs a) {
     constexpr int S = APPLY_STEP;
     __shared__ short2 lds[3][S][APPLY_TILES];
+    __shared__ double2 etab[64];
+    if (threadIdx.x < 64) etab[threadIdx.x] = EXP2_TAB64[threadIdx.x];
+    __syncthreads();
     const int b = threadIdx.x / APPLY_TILES;
     const int lane = threadIdx.x % APPLY_TILES;
     const int64_t G = a.G;
@@ -1182,44 +1456,31 @@ __global__ void __launch_bounds__(192, MM_APPLY_MINB) comp_apply_kernel(CompArgs
     // M loads or steps
     const bool quiet = __all(!valid || a.cnt[b][g] == 0);
     if (quiet) {
-        gain = exp10(neg_div20(att));
+        gain = MM_GAIN(att);
         gain_att = att;
     }
     const uint32_t G32 = (uint32_t)G, gl = valid ? (uint32_t)g : 0u;
-    const int last = max(len - 1, 0);
-    double m1[S], m2[S];
-    short2 v1[S], v2[S];
+    const uint32_t last = (uint32_t)max(len - 1, 0);
+    const short2 *Xl = X + gl;       // this lane's tile, row 0
+    const double *Ml = Mp + e0;      // this lane's column, its tile's row 0
     // rows past the tile's frames hold M = 0 (comp_rms): identity steps whose
     // output is unused; samples are clamped to the tile
-    auto load = [&](int n0, double (&m)[S], short2 (&v)[S]) {
+    auto load = [&](int n0, double (&m)[S], short2 (&v)[S], bool with_m) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < S; ++j) {
-            m[j] = Mp[e0 + (uint32_t)min(n0 + j, T - 1) * GS32];
-            v[j] = X[(uint32_t)min(n0 + j, last) * G32 + gl];
+            if (with_m) m[j] = Ml[(size_t)min(n0 + j, T - 1) * GS32];  // (uniform row)
+            v[j] = Xl[(size_t)min((uint32_t)(n0 + j), last) * G32];
         }
     };
-    load(0, m1, v1);
-    load(S, m2, v2);
-    for (int n0 = 0; n0 < T; n0 += S) {
-        // this group: v1, m1; next: m2, v2
-        short2 v[S];
-        double m[S];
-#pragma unroll
-        for (int j = 0; j < S; ++j) {
-            v[j] = v1[j];
-            m[j] = m1[j];
-            v1[j] = v2[j];
-            m1[j] = m2[j];
-        }
+    // one group of S frames from its buffers (m, v), then the buffers refilled with
+    // the group two ahead: two groups unrolled per iteration, so the buffers never
+    // rotate through register copies
+    auto group = [&](int n0, double (&m)[S], short2 (&v)[S]) __attribute__((always_inline)) {
         double gj[S];
         if (quiet) {  // wave-uniform: only the samples stream
 #pragma unroll
-            for (int j = 0; j < S; ++j) {
-                v2[j] = X[(uint32_t)min(n0 + 2 * S + j, last) * G32 + gl];
-                gj[j] = gain;
-            }
+            for (int j = 0; j < S; ++j) gj[j] = gain;
         } else {
-            load(n0 + 2 * S, m2, v2);
             double at[S];
             bool same = true;
 #pragma unroll
@@ -1237,7 +1498,7 @@ __global__ void __launch_bounds__(192, MM_APPLY_MINB) comp_apply_kernel(CompArgs
 #ifdef MM_APPLY_NOEXP  // timing experiment only (wrong gains)
                     gj[j] = 1.0 + neg_div20(at[j]);
 #else
-                    gj[j] = exp10(neg_div20(at[j]));  // db_to_float(-att); exp10(-0) == 1 exactly
+                    gj[j] = MM_GAIN(at[j]);  // db_to_float(-att); exactly 1 at att == 0
 #endif
                 gain = gj[S - 1];
                 gain_att = at[S - 1];
@@ -1250,6 +1511,7 @@ __global__ void __launch_bounds__(192, MM_APPLY_MINB) comp_apply_kernel(CompArgs
             s.y = audioop_mul(s.y, gj[j]);
             lds[b][j][lane] = s;
         }
+        load(n0 + 2 * S, m, v, !quiet);
         lds_barrier();
         for (int p = threadIdx.x; p < S * APPLY_TILES; p += 3 * APPLY_TILES) {
             const int j = p / APPLY_TILES, tl = p % APPLY_TILES;
@@ -1263,6 +1525,14 @@ __global__ void __launch_bounds__(192, MM_APPLY_MINB) comp_apply_kernel(CompArgs
             }
         }
         lds_barrier();
+    };
+    double mA[S], mB[S];
+    short2 vA[S], vB[S];
+    load(0, mA, vA, !quiet);
+    load(S, mB, vB, !quiet);
+    for (int n0 = 0; n0 < T; n0 += 2 * S) {
+        group(n0, mA, vA);
+        if (n0 + S < T) group(n0 + S, mB, vB);
     }
 }
 

@@ -11,8 +11,10 @@ __device__ __forceinline__ int16_t audioop_mul(int16_t x, double g) {
     // audioop's "v > 32767 -> 32767; v < -32767 -> -32768; floor(v)" equals
     // floor(v) clamped to [-32768, 32767] (v in (-32768, -32767) floors to
     // -32768 too); min/max instead of branches
-    const double v = floor(__builtin_fmin(__builtin_fmax((double)x * g, -32768.0), 32767.0));
-    return (int16_t)(int32_t)v;
+    // (clamping the floored integer: the bounds are integers, so clamp(floor(v)) ==
+    // floor(clamp(v)); |x g| <= 32768 here, inside v_cvt_i32_f64's range)
+    const int32_t i = (int32_t)floor((double)x * g);
+    return (int16_t)min(max(i, -32768), 32767);
 }
 
 __device__ __forceinline__ int16_t sat16(int32_t v) {

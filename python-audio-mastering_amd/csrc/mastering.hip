@@ -464,6 +464,7 @@ static int solve_geometry(const mm_job *j, mm_solve_geom *g) {
     g->tps = std::max(1, std::min((j->comp_super + T / 2) / T, DESC_MAX_TPS));  // (comp_describe: 64 TPS threads)
     g->chunks = (G + K - 1) / K;
     g->cols_per_chunk = (((int64_t)K + g->tps - 1) / g->tps + 63) / 64 * 64;
+    g->walk_block = WB;
     g->tile_rows = (T + WB - 1) / WB * WB;
     g->rows = g->tps * g->tile_rows + WALK_PAD;
     g->chunk_plane_bytes = (int64_t)g->rows * g->cols_per_chunk * 8;
@@ -1621,52 +1622,87 @@ int mm_hop_energies(mm_ctx *c, const double *carry_in_host, double *seg_energy_h
 // on the device (gate_kernel over the given block -> segment ranges), and finalize
 // reads the gain from device memory.  One host synchronisation before (the
 // envelope solve's convergence check, as mm_hop_energies) and one after (L).
-int mm_shard_loudness_device(mm_ctx *c, const double *carry_in_host, int64_t n_global_segs, int64_t seg_offset,
-                             int64_t n_blocks, const int32_t *blk_s0_host, const int32_t *blk_s1_host,
-                             double block_scale, double target, void *d_out, double *loudness_host) {
+// Time-sharded loudness with the energy vector in HBM, in three steps a caller can
+// compose with any collective between them (the library's communicator, or
+// torch.distributed over the same device buffer):
+//  1. mm_shard_energies_device: zero the caller's whole-track vector d_full and write
+//     this rank's segment energies at seg_offset (a rank's segments are consecutive
+//     global ones);
+//  2. a sum all-reduce of d_full over the ranks (mm_allreduce_sum_f64_device);
+//  3. mm_gate_finalize_device: pyloudnorm's gating of the whole track on the device,
+//     the gain towards `target` applied by finalize straight from device memory;
+//     returns L and the gain it applied.
+int mm_shard_energies_device(mm_ctx *c, const double *carry_in_host, int64_t n_global_segs, int64_t seg_offset,
+                             double *d_full) {
     if (!c || !c->staged) return set_err(c, MM_ERR_STATE, "no staged job");
     const int64_t nl = c->job.n_segs;
-    if (n_global_segs < 1 || seg_offset < 0 || seg_offset + nl > n_global_segs || n_blocks < 1 || !blk_s0_host ||
-        !blk_s1_host || !loudness_host)
-        return set_err(c, MM_ERR_ARG, "shard loudness: bad segment or block geometry");
-    for (int64_t b = 0; b < n_blocks; ++b)
-        if (blk_s0_host[b] < 0 || blk_s1_host[b] < blk_s0_host[b] || blk_s1_host[b] > n_global_segs)
-            return set_err(c, MM_ERR_ARG, "shard loudness: block %lld has segments [%d, %d) outside [0, %lld)",
-                           (long long)b, blk_s0_host[b], blk_s1_host[b], (long long)n_global_segs);
-    double *full, *gout;
-    int32_t *s0, *s1;
-    RET(get_buf(c, "shard_seg", (size_t)n_global_segs, &full));
-    RET(get_buf(c, "shard_gate", 2, &gout));
-    RET(get_buf(c, "shard_blk0", (size_t)n_blocks, &s0));
-    RET(get_buf(c, "shard_blk1", (size_t)n_blocks, &s1));
-    HIPCHK(c, hipMemsetAsync(full, 0, (size_t)n_global_segs * sizeof(double), c->stream));
+    if (!d_full || n_global_segs < 1 || seg_offset < 0 || seg_offset + nl > n_global_segs)
+        return set_err(c, MM_ERR_ARG, "shard energies: segments [%lld, %lld) outside [0, %lld)",
+                       (long long)seg_offset, (long long)(seg_offset + nl), (long long)n_global_segs);
+    HIPCHK(c, hipMemsetAsync(d_full, 0, (size_t)n_global_segs * sizeof(double), c->stream));
     if (c->G > 0 && nl > 0) {
         double *seg;
         RET(kweight_launch(c, carry_in_host, nullptr, &seg));
-        HIPCHK(c, hipMemcpyAsync(full + seg_offset, seg, (size_t)nl * sizeof(double), hipMemcpyDeviceToDevice,
+        HIPCHK(c, hipMemcpyAsync(d_full + seg_offset, seg, (size_t)nl * sizeof(double), hipMemcpyDeviceToDevice,
                                  c->stream));
     }
     bool conv;
-    RET(chain_check(c, &conv));
-    if (c->comm && c->nranks > 1) {
-        ncclResult_t r = ncclAllReduce(full, full, (size_t)n_global_segs, ncclDouble, ncclSum, c->comm, c->stream);
-        if (r != ncclSuccess) return set_err(c, MM_ERR_RCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
-    }
+    RET(chain_check(c, &conv));  // (synchronises the stream: d_full is complete on return)
+    return MM_OK;
+}
+
+int mm_gate_finalize_device(mm_ctx *c, const double *d_full, int64_t n_global_segs, int64_t n_blocks,
+                            const int32_t *blk_s0_host, const int32_t *blk_s1_host, double block_scale,
+                            double target, void *d_out, double *loudness_gain_host) {
+    if (!c || !c->staged) return set_err(c, MM_ERR_STATE, "no staged job");
+    if (!d_full || n_global_segs < 1 || n_blocks < 1 || !blk_s0_host || !blk_s1_host || !loudness_gain_host)
+        return set_err(c, MM_ERR_ARG, "gate: bad segment or block geometry");
+    for (int64_t b = 0; b < n_blocks; ++b)
+        if (blk_s0_host[b] < 0 || blk_s1_host[b] < blk_s0_host[b] || blk_s1_host[b] > n_global_segs)
+            return set_err(c, MM_ERR_ARG, "gate: block %lld has segments [%d, %d) outside [0, %lld)",
+                           (long long)b, blk_s0_host[b], blk_s1_host[b], (long long)n_global_segs);
+    double *gout;
+    int32_t *s0, *s1;
+    RET(get_buf(c, "shard_gate", 2, &gout));
+    RET(get_buf(c, "shard_blk0", (size_t)n_blocks, &s0));
+    RET(get_buf(c, "shard_blk1", (size_t)n_blocks, &s1));
     HIPCHK(c, hipMemcpyAsync(s0, blk_s0_host, (size_t)n_blocks * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(s1, blk_s1_host, (size_t)n_blocks * sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
     GateArgs ga{};
     ga.n_blocks = n_blocks;
     ga.blk_s0 = s0;
     ga.blk_s1 = s1;
-    ga.seg = full;
+    ga.seg = d_full;
     ga.scale = block_scale;
     ga.target = target;
     ga.out = gout;
     RET(launch(c, "gate", gate_kernel, dim3(1), dim3(GATE_THREADS), 0, ga));
     RET(finalize(c, 1.0, gout + 1, 1, d_out));
-    HIPCHK(c, hipMemcpyAsync(loudness_host, gout, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    // L and the gain finalize applied (gate.hip's device expression, not a host recomputation)
+    HIPCHK(c, hipMemcpyAsync(loudness_gain_host, gout, 2 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return MM_OK;
+}
+
+// Steps 1-3 with the library's own communicator.  `world` is the plan's rank count:
+// a multi-rank plan needs this context's RCCL communicator over exactly that many
+// ranks, or every rank would gate only its own part of the vector (and return a
+// different, wrong loudness) — refused instead.
+int mm_shard_loudness_device(mm_ctx *c, const double *carry_in_host, int64_t n_global_segs, int64_t seg_offset,
+                             int64_t n_blocks, const int32_t *blk_s0_host, const int32_t *blk_s1_host,
+                             double block_scale, double target, int32_t world, void *d_out,
+                             double *loudness_gain_host) {
+    if (!c) return MM_ERR_ARG;
+    if (world < 1) return set_err(c, MM_ERR_ARG, "shard loudness: world %d", world);
+    if (world > 1 && (!c->comm || c->nranks != world))
+        return set_err(c, MM_ERR_STATE, "shard loudness: a %d-rank plan needs this context's communicator over %d "
+                       "ranks (have %d)", world, world, c->comm ? c->nranks : 0);
+    double *full;
+    RET(get_buf(c, "shard_seg", (size_t)std::max<int64_t>(n_global_segs, 1), &full));
+    RET(mm_shard_energies_device(c, carry_in_host, n_global_segs, seg_offset, full));
+    if (world > 1) RET(mm_allreduce_sum_f64_device(c, full, n_global_segs));
+    return mm_gate_finalize_device(c, full, n_global_segs, n_blocks, blk_s0_host, blk_s1_host, block_scale, target,
+                                   d_out, loudness_gain_host);
 }
 
 int mm_finalize(mm_ctx *c, double gain_linear, int use_gain, void *d_out) {
@@ -1755,6 +1791,32 @@ int mm_allreduce_sum_f64(mm_ctx *c, double *host_buf, int64_t n) {
     ncclResult_t r = ncclAllReduce(d, d, (size_t)n, ncclDouble, ncclSum, c->comm, c->stream);
     if (r != ncclSuccess) return set_err(c, MM_ERR_RCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
     HIPCHK(c, hipMemcpyAsync(host_buf, d, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return MM_OK;
+}
+
+// Device-pointer collectives on the context's stream: no host
+// staging; the buffers must live on this context's device.  Synchronous on return.
+int mm_allreduce_sum_f64_device(mm_ctx *c, double *d_buf, int64_t n) {
+    if (!c) return MM_ERR_ARG;
+    if (n < 0 || (n > 0 && !d_buf)) return set_err(c, MM_ERR_ARG, "all-reduce: bad buffer");
+    if (!c->comm) return set_err(c, MM_ERR_STATE, "communicator not initialised");
+    if (n > 0) {
+        ncclResult_t r = ncclAllReduce(d_buf, d_buf, (size_t)n, ncclDouble, ncclSum, c->comm, c->stream);
+        if (r != ncclSuccess) return set_err(c, MM_ERR_RCCL, "ncclAllReduce: %s", ncclGetErrorString(r));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return MM_OK;
+}
+
+int mm_allgather_f64_device(mm_ctx *c, const double *d_in, double *d_out, int64_t n) {
+    if (!c) return MM_ERR_ARG;
+    if (n < 0 || (n > 0 && (!d_in || !d_out))) return set_err(c, MM_ERR_ARG, "all-gather: bad buffers");
+    if (!c->comm) return set_err(c, MM_ERR_STATE, "communicator not initialised");
+    if (n > 0) {
+        ncclResult_t r = ncclAllGather(d_in, d_out, (size_t)n, ncclDouble, c->comm, c->stream);
+        if (r != ncclSuccess) return set_err(c, MM_ERR_RCCL, "ncclAllGather: %s", ncclGetErrorString(r));
+    }
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return MM_OK;
 }

@@ -30,6 +30,8 @@ DEFAULT_TILE = 225     # divides 30 s chunks at 11.025/22.05/44.1/48/88.2/96/192
                        # 225 fastest on C2, P_HOT, C3 and C5)
 NOCOMP_TILE = 125      # tile of jobs without the multiband compressor (EQ / K-weighting lanes)
 OPS_TILE = 125         # tile of the per-stage operators' look-back tables (== OPS_TILE in csrc/ops.hip)
+WALK_BLOCK = 25        # rows per walk load block of the compressor's M plane (MM_WALK_B; the library reports
+                       # it as mm_solve_geom.walk_block, checked in tests/test_abi.py)
 
 EQ_KEYS = ("bass_boost", "mid_cut", "presence_boost", "treble_boost")
 BAND_TIMES = ((10.0, 200.0), (5.0, 150.0), (1.0, 50.0))  # (attack, release) ms, AME:207-209
@@ -89,14 +91,14 @@ def check_chunk_geometry(bounds, nominal: int, rate: int, multiband: bool):
 def choose_tile(chunk_frames: int, preferred: int | None = None) -> int:
     """The tile length of a chunk: `preferred` (DEFAULT_TILE) when it divides the chunk,
     else the divisor in [64, 512] nearest to it, counting the walk-block padding of the
-    compressor's plane rows (tiles are padded to whole 25-row blocks) as distance."""
+    compressor's plane rows (tiles are padded to whole WALK_BLOCK-row blocks) as distance."""
     preferred = preferred or DEFAULT_TILE
     if chunk_frames % preferred == 0:
         return preferred
     best, best_cost = 0, None
     for t in range(64, 513):
         if chunk_frames % t == 0:
-            cost = abs(t - preferred) / preferred + ((t + 24) // 25 * 25 - t) / t
+            cost = abs(t - preferred) / preferred + ((t + WALK_BLOCK - 1) // WALK_BLOCK * WALK_BLOCK - t) / t
             if best_cost is None or cost < best_cost:
                 best, best_cost = t, cost
     if not best:

@@ -170,6 +170,14 @@ class TorchCollectives:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
         return t.cpu().numpy()
 
+    def all_reduce_sum_device(self, t):
+        """In-place sum all-reduce of a device tensor (RCCL over xGMI with "nccl"), no
+        host copies; complete on return (the library reads the buffer next)."""
+        import torch
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.group)
+        torch.cuda.current_stream(t.device).synchronize()
+        return t
+
 
 def rccl_unique_id() -> bytes:
     """A fresh RCCL unique id (128 bytes) for mm_comm_init; rank 0 makes it and
@@ -213,6 +221,18 @@ class LibraryCollectives:
         self.ctx.check(self.ctx.lib.mm_allreduce_sum_f64(self.ctx.ptr, v.ctypes.data_as(native.c_double_p),
                                                          v.size), "mm_allreduce_sum_f64")
         return v
+
+    def all_reduce_sum_device(self, d_buf: int, n: int):
+        """In-place sum all-reduce of n doubles at device address d_buf (this context's
+        device), no host staging (mm_allreduce_sum_f64_device)."""
+        self.ctx.check(self.ctx.lib.mm_allreduce_sum_f64_device(self.ctx.ptr, ctypes.c_void_p(d_buf), int(n)),
+                       "mm_allreduce_sum_f64_device")
+
+    def all_gather_device(self, d_in: int, d_out: int, n: int):
+        """All-gather of n doubles per rank between device buffers (d_out: world * n)."""
+        self.ctx.check(self.ctx.lib.mm_allgather_f64_device(self.ctx.ptr, ctypes.c_void_p(d_in),
+                                                            ctypes.c_void_p(d_out), int(n)),
+                       "mm_allgather_f64_device")
 
 
 class TorchLikeHost:
@@ -269,21 +289,49 @@ class GpuBackend:
                                                     e.ctypes.data_as(native.c_double_p)), "mm_hop_energies")
         return e
 
-    def shard_loudness_device(self, carry: np.ndarray, plan: "RankPlan", target: float, d_out: int) -> float:
+    def shard_loudness_device(self, carry: np.ndarray, plan: "RankPlan", target: float, d_out: int):
         """Steps 3-5 with the energy vector kept in HBM (mm_shard_loudness_device): this
         rank's segment energies into the whole-track vector, the RCCL sum all-reduce
-        in place (the context's communicator), device gating and the device gain into
-        mm_finalize.  Returns the whole track's loudness."""
+        in place (the context's communicator, which must span plan.world ranks), device
+        gating and the device gain into mm_finalize.  Returns (L, the gain applied)."""
         c = np.ascontiguousarray(carry, dtype=np.float64)
         n_glob = len(plan.seg_bounds) - 1
         s0, s1 = block_segments(plan)
-        L = ctypes.c_double(0.0)
+        lg = np.zeros(2)
         self.ctx.check(self.ctx.lib.mm_shard_loudness_device(
             self.ctx.ptr, c.ctypes.data_as(native.c_double_p), n_glob, int(plan.local_to_global[0]), len(s0),
             s0.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), s1.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
-            float(plan.block_scale), float(target), ctypes.c_void_p(d_out), ctypes.byref(L)),
-            "mm_shard_loudness_device")
-        return float(L.value)
+            float(plan.block_scale), float(target), int(plan.world), ctypes.c_void_p(d_out),
+            lg.ctypes.data_as(native.c_double_p)), "mm_shard_loudness_device")
+        return float(lg[0]), float(lg[1])
+
+    def shard_energies_device(self, carry: np.ndarray, plan: "RankPlan", d_full: int):
+        """Step 3 into a caller's device vector of the whole track's segments."""
+        c = np.ascontiguousarray(carry, dtype=np.float64)
+        self.ctx.check(self.ctx.lib.mm_shard_energies_device(
+            self.ctx.ptr, c.ctypes.data_as(native.c_double_p), len(plan.seg_bounds) - 1,
+            int(plan.local_to_global[0]), ctypes.c_void_p(d_full)), "mm_shard_energies_device")
+
+    def gate_finalize_device(self, d_full: int, plan: "RankPlan", target: float, d_out: int):
+        """Step 5 from the summed device vector: (L, the gain applied)."""
+        s0, s1 = block_segments(plan)
+        lg = np.zeros(2)
+        self.ctx.check(self.ctx.lib.mm_gate_finalize_device(
+            self.ctx.ptr, ctypes.c_void_p(d_full), len(plan.seg_bounds) - 1, len(s0),
+            s0.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), s1.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+            float(plan.block_scale), float(target), ctypes.c_void_p(d_out), lg.ctypes.data_as(native.c_double_p)),
+            "mm_gate_finalize_device")
+        return float(lg[0]), float(lg[1])
+
+    def shard_loudness_torch(self, carry: np.ndarray, plan: "RankPlan", target: float, d_out: int, coll):
+        """Steps 3-5 with torch.distributed ("nccl" = RCCL) summing the library's energy
+        vector in place in HBM: the vector is a torch tensor on this context's device."""
+        import torch
+        full = torch.zeros(len(plan.seg_bounds) - 1, dtype=torch.float64,
+                           device=torch.device("cuda", self.ctx.device))
+        self.shard_energies_device(carry, plan, full.data_ptr())
+        coll.all_reduce_sum_device(full)
+        return self.gate_finalize_device(full.data_ptr(), plan, target, d_out)
 
     def finalize(self, gain: float, use_gain: bool, d_out: int):
         self.ctx.check(self.ctx.lib.mm_finalize(self.ctx.ptr, float(gain), int(use_gain), ctypes.c_void_p(d_out)),
@@ -304,12 +352,26 @@ def master_time_sharded(backend, plan: RankPlan, params: dict, d_in, d_out, coll
         zl = coll.all_gather(np.concatenate([z, [float(plan.frames)]]))
         carry = compose_carry(zl[:, :4], zl[:, 4].astype(np.int64), plan.rate, plan.rank)
         l2g = plan.local_to_global
-        if (isinstance(coll, (LibraryCollectives, LocalCollectives)) and hasattr(backend, "shard_loudness_device")
-                and len(l2g) and np.all(np.diff(l2g) == 1)):
-            # the library's own communicator (or none): energies, all-reduce, gating and
-            # gain stay on the device (a rank's segments are consecutive global ones)
-            L = backend.shard_loudness_device(carry, plan, float(lufs), d_out)
-            gain = 10.0 ** ((float(lufs) - L) / 20.0)
+        if not (len(l2g) and np.all(np.diff(l2g) == 1)):  # plan_time_shards always makes them consecutive
+            raise ValueError("a rank's loudness segments must be consecutive global segments")
+        # the path depends only on the collective's kind and the plan, the same on every rank
+        if isinstance(coll, LibraryCollectives) and (coll.ctx is not getattr(backend, "ctx", None)
+                                                     or coll.world != plan.world):
+            raise ValueError("LibraryCollectives must wrap the backend's own context (its RCCL communicator) "
+                             "over the plan's world")
+        mode = None
+        if hasattr(backend, "shard_loudness_device"):
+            if isinstance(coll, LibraryCollectives) or (isinstance(coll, LocalCollectives) and plan.world == 1):
+                mode = "library"
+            elif isinstance(coll, TorchCollectives) and coll.device == "cuda":
+                mode = "torch"
+        if mode is not None:
+            # energies, all-reduce, gating and gain stay on the device; the gain returned
+            # is the one finalize applied (gate.hip), not a host recomputation
+            if mode == "library":
+                L, gain = backend.shard_loudness_device(carry, plan, float(lufs), d_out)
+            else:
+                L, gain = backend.shard_loudness_torch(carry, plan, float(lufs), d_out, coll)
             return {"loudness": L, "gain_linear": gain, "frames": plan.frames, "f0": plan.f0, "f1": plan.f1,
                     "device_gate": True}
         local = backend.hop_energies(carry)

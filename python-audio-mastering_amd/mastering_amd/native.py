@@ -62,11 +62,11 @@ class MMResult(ctypes.Structure):
 
 class MMSolveGeom(ctypes.Structure):
     _fields_ = [("tps", ctypes.c_int32), ("tile_rows", ctypes.c_int32), ("rows", ctypes.c_int32),
-                ("_pad", ctypes.c_int32), ("cols_per_chunk", ctypes.c_int64), ("chunks", ctypes.c_int64),
+                ("walk_block", ctypes.c_int32), ("cols_per_chunk", ctypes.c_int64), ("chunks", ctypes.c_int64),
                 ("chunk_plane_bytes", ctypes.c_int64), ("plane_bytes", ctypes.c_int64)]
 
 
-ABI_VERSION = 2  # MM_ABI_VERSION of include/mastering.h
+ABI_VERSION = 3  # MM_ABI_VERSION of include/mastering.h
 
 
 class MMWavInfo(ctypes.Structure):
@@ -78,6 +78,8 @@ class MMWavInfo(ctypes.Structure):
 EXPORTS = ("mm_create", "mm_destroy", "mm_last_error", "mm_sync", "mm_version", "mm_source_sha", "mm_master",
            "mm_master_device",
            "mm_stage_chunks", "mm_kweight_range_end", "mm_hop_energies", "mm_shard_loudness_device",
+           "mm_shard_energies_device", "mm_gate_finalize_device", "mm_allreduce_sum_f64_device",
+           "mm_allgather_f64_device",
            "mm_gate_loudness", "mm_finalize",
            "mm_read_mix", "mm_timing", "mm_kernel_stats", "mm_comm_unique_id", "mm_comm_init", "mm_comm_destroy",
            "mm_allreduce_sum_f64", "mm_allgather_f64", "mm_wav_probe", "mm_master_wav",
@@ -120,9 +122,14 @@ def load():
             "mm_master_wav": ([vp, P(MMJob), ctypes.c_char_p, ctypes.c_char_p, P(MMResult)], ctypes.c_int),
             "mm_kweight_range_end": ([vp, c_double_p], ctypes.c_int),
             "mm_hop_energies": ([vp, c_double_p, c_double_p], ctypes.c_int),
+            "mm_shard_energies_device": ([vp, c_double_p, ctypes.c_int64, ctypes.c_int64, vp], ctypes.c_int),
+            "mm_gate_finalize_device": ([vp, vp, ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(ctypes.c_int32),
+                                         ctypes.POINTER(ctypes.c_int32), ctypes.c_double, ctypes.c_double, vp,
+                                         c_double_p], ctypes.c_int),
             "mm_shard_loudness_device": ([vp, c_double_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                           ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
-                                          ctypes.c_double, ctypes.c_double, vp, c_double_p], ctypes.c_int),
+                                          ctypes.c_double, ctypes.c_double, ctypes.c_int32, vp, c_double_p],
+                                         ctypes.c_int),
             "mm_gate_loudness": ([P(MMJob), c_double_p, c_double_p], ctypes.c_int),
             "mm_finalize": ([vp, ctypes.c_double, ctypes.c_int, vp], ctypes.c_int),
             "mm_read_mix": ([vp, P(ctypes.c_int16)], ctypes.c_int),
@@ -134,6 +141,8 @@ def load():
             "mm_comm_destroy": ([vp], ctypes.c_int),
             "mm_allreduce_sum_f64": ([vp, c_double_p, ctypes.c_int64], ctypes.c_int),
             "mm_allgather_f64": ([vp, c_double_p, c_double_p, ctypes.c_int64], ctypes.c_int),
+            "mm_allreduce_sum_f64_device": ([vp, vp, ctypes.c_int64], ctypes.c_int),
+            "mm_allgather_f64_device": ([vp, vp, vp, ctypes.c_int64], ctypes.c_int),
             "mm_op_pcm_to_float": ([vp, vp, ctypes.c_int64, vp], ctypes.c_int),
             "mm_op_saturation": ([vp, ctypes.c_int, vp, ctypes.c_int64, ctypes.c_double, vp], ctypes.c_int),
             "mm_op_stereo_width": ([vp, ctypes.c_int, vp, ctypes.c_int64, ctypes.c_double, vp], ctypes.c_int),

@@ -104,7 +104,8 @@ def test_solve_geometry_up_to_2_31_frames(rate):
         assert lib.mm_solve_geometry(ctypes.byref(j), ctypes.byref(g)) == 0, frames
         assert g.chunks == -(-frames // chunk)
         assert g.cols_per_chunk % 64 == 0 and g.cols_per_chunk * g.tps >= chunk // tile
-        assert g.tile_rows >= tile and g.tile_rows % 25 == 0
+        assert g.walk_block == design.WALK_BLOCK  # choose_tile's padding model is the library's
+        assert g.tile_rows >= tile and g.tile_rows % g.walk_block == 0
         assert 0 < g.chunk_plane_bytes < 2**31
         assert g.plane_bytes == 3 * g.chunks * g.chunk_plane_bytes
         if prev is not None:  # per-chunk geometry does not depend on the length
