@@ -124,180 +124,6 @@ __device__ __forceinline__ double *chunk_plane(const CompArgs &a, int b, int64_t
 #ifndef MM_RMS_MINB
 #define MM_RMS_MINB 1
 #endif
-#ifdef MM_RMS_V1  // round-4 lane mapping (A/B builds)
-__global__ void __launch_bounds__(256, MM_RMS_MINB) comp_rms_kernel(CompArgs a) {
-    const int b = blockIdx.y;
-    const int64_t wv = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int kc = (int)(wv % a.TPS);
-    const int64_t sc = (wv / a.TPS) * 64 + (threadIdx.x & 63);
-    const int64_t cc = sc / a.SPC;
-    const int64_t jt = (sc - cc * a.SPC) * a.TPS + kc;
-    const int64_t g = cc * a.K + jt;
-    if (jt >= a.K || g >= a.G) return;  // past the chunk's tiles (its last super-tile) or the track
-    const short2 *x = a.band[b];
-    const int look = a.look[b];
-    const int T = a.T;
-    const uint32_t G = (uint32_t)a.G, g32 = (uint32_t)g;
-    const int64_t f0 = g * T;
-    const int64_t chunk0 = (g / a.K) * a.K * T;
-    const int len = (int)min((int64_t)T, a.N_proc - f0);
-    // S over [lo0, f0): the look / T whole tiles before this one plus the last
-    // look % T frames of the one before them, from the crossover's per-tile sums
-    // (tiles never straddle a chunk start, so the chunk clamp is per tile)
-    const int64_t lo0 = max(chunk0, f0 - look);
-    double S = 0.0;
-    {
-        const int kf = look / T;
-        for (int t = 1; t <= kf; ++t)
-            if ((g - t) * T >= chunk0) S += a.E[b][g - t];
-        if (look % T != 0 && (g - kf - 1) * T >= chunk0) S += a.tail[b][g - kf - 1];
-    }
-    // drop frames: d = f - look for f >= chunk0 + look; the first `skip` frames drop nothing
-    const int64_t d_first = max(f0 - look, chunk0);
-    const int skip = (int)(d_first - (f0 - look));
-    const uint32_t gd = (uint32_t)(d_first / T);
-    const int nd = (int)(d_first - (int64_t)gd * T);
-    const int ch = a.ch;
-    double n = (double)((f0 - lo0) * ch);
-    float inv = n > 0.0 ? __builtin_amdgcn_rcpf((float)n) : 0.f;  // (an estimate's factor only)
-    const uint32_t r0 = a.r0[b];
-    const double *lut = a.lut[b];
-    const double Rf = a.release_frames[b], rR = a.rcp_release[b];
-    constexpr uint32_t GS32 = 64;  // elements per row of a column block
-    double *Mo = chunk_plane(a, b, cc);
-    uint32_t e = col_elem(a, sc) + (uint32_t)(kc * a.TP) * GS32;  // row k*TP of column s
-    int i_proc = 0, active = 0;
-    uint32_t rmx = 0;
-    struct Pair {
-        short2 in, drop;
-    };
-    auto ld = [&](int i) {
-        i = min(i, len - 1);
-        Pair p;
-        p.in = x[(uint32_t)i * G + g32];
-        int k = nd + max(i - skip, 0);  // < 2T
-        const int wrap = k >= T ? 1 : 0;
-        k -= wrap * T;
-        p.drop = x[(uint32_t)k * G + gd + (uint32_t)wrap];
-        return p;
-    };
-    // st: BoolTag<true> when no lane of the wave is in a chunk's first `look` frames
-    // (every wave but the few holding a chunk's first tiles): the window slides, n is fixed
-    auto rms_step = [&](Pair p, auto st) __attribute__((always_inline)) {
-        const uint32_t r = rms_exact(S, n, inv);
-        active += r >= r0 ? 1 : 0;
-        rmx = max(rmx, r);
-        if constexpr (decltype(st)::value) {
-            S += (double)frame_energy(p.in) - (double)frame_energy(p.drop);
-        } else {
-            const bool drops = i_proc >= skip;
-            S += (double)frame_energy(p.in) - (drops ? (double)frame_energy(p.drop) : 0.0);
-            if (!drops) {  // window still growing (first `look` frames of a chunk only)
-                n += ch;
-                inv = __builtin_amdgcn_rcpf((float)n);
-            }
-            ++i_proc;
-        }
-        return r;
-    };
-    // blocks of RMS_B frames: loads MM_RMS_NB blocks ahead; the block's M gathers
-    // are stored after the next block's rms (their latency behind it)
-    constexpr int B = RMS_B, NB = MM_RMS_NB;
-    Pair buf[NB][B];
-    double mq[B];
-    int pn = 0;  // rows of the pending block (its gathers in flight)
-    // (max,+) release summary of the tile for the pass-0 guesses: ce = the per-frame
-    // walk E <- max(M, E - M/R) from E = 0 (every attack an instant clamp; M/R
-    // correctly rounded, so ce is bit-exact: e_fold_tile), De ~ the tile's release
-    double ce = 0.0, De = 0.0;
-    // store the pending block: whole (every block but a partial last one) or its pn rows
-    auto flush = [&](bool whole) __attribute__((always_inline)) {
-#pragma unroll
-        for (int j = 0; j < B; ++j)
-            if (whole || j < pn) {
-#ifndef MM_RMS_NOSTORE  // (timing experiment only: no M plane)
-                Mo[e + (uint32_t)j * GS32] = mq[j];
-#endif
-                const double d = div_cr(mq[j], Rf, rR);
-                ce = fmax(mq[j], ce - d);
-                De += d;
-            }
-        e += (uint32_t)pn * GS32;
-    };
-    auto run = [&](auto st) __attribute__((always_inline)) {
-#pragma unroll
-        for (int k = 0; k < NB; ++k) {
-#pragma unroll
-            for (int j = 0; j < B; ++j) buf[k][j] = ld(k * B + j);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        // nv: frames of the block (B except a partial last one); constant at the
-        // full-block call sites, so their guards fold away
-        auto block = [&](int k, int q, int nv) __attribute__((always_inline)) {
-            uint32_t r[B];
-#pragma unroll
-            for (int j = 0; j < B; ++j) r[j] = j < nv ? rms_step(buf[k][j], st) : 0u;
-            double m[B];
-#ifdef MM_RMS_NOGATHER  // timing experiment only (wrong M)
-#pragma unroll
-            for (int j = 0; j < B; ++j) m[j] = (double)r[j];
-#else
-#pragma unroll
-            for (int j = 0; j < B; ++j) m[j] = lut[r[j]];
-#endif
-            __builtin_amdgcn_sched_barrier(0);
-            if (q > 0) flush(true);  // (the block before a block is whole)
-#pragma unroll
-            for (int j = 0; j < B; ++j) buf[k][j] = ld((q + NB) * B + j);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int j = 0; j < B; ++j) mq[j] = m[j];
-            pn = nv;
-        };
-        const int nfull = len / B, ntail = len - nfull * B;
-        int q = 0;
-        for (; q + NB <= nfull; q += NB) {
-#pragma unroll
-            for (int k = 0; k < NB; ++k) block(k, q + k, B);
-        }
-#pragma unroll
-        for (int k = 0; k < NB; ++k)
-            if (q + k < nfull) block(k, q + k, B);
-        if (ntail) {
-#pragma unroll
-            for (int k = 0; k < NB; ++k)
-                if (k == nfull % NB) block(k, nfull, ntail);
-        }
-        flush(false);
-    };
-    if (len > 0) {
-        if (__all(skip == 0)) run(BoolTag<true>{});
-        else run(BoolTag<false>{});
-    }
-    // rows past the tile's frames (a partial last tile, the padding to TP): M = 0
-    // (identity steps)
-    for (int i = max(len, 0); i < a.TP; ++i, e += GS32) Mo[e] = 0.0;
-    a.cnt[b][g] = active;
-    a.mmax[b][g] = lut[rmx];
-    {  // active tiles of the column block (comp_describe ranks the chunk's active tiles from them)
-        const int na = (int)__popcll(__ballot(active != 0));
-        if (__lane_id() == __builtin_amdgcn_readfirstlane(__lane_id()) && na)
-            atomicAdd(a.cbtot[b] + (sc >> 6), na);
-    }
-    reinterpret_cast<double2 *>(a.ced[b])[g] = make_double2(ce, De);
-    // per-chunk active count (statistics): one atomic per wave when all 64 lanes
-    // are live (lanes past the chunk's tiles or G exited above; the wave's tiles
-    // share a chunk)
-    const int c = (int)cc;
-    if (__ballot(1) == ~0ull) {
-        int v = active;
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-        if (__lane_id() == 0 && v) atomicAdd(a.total[b] + c, v);
-    } else if (active) {
-        atomicAdd(a.total[b] + c, active);
-    }
-}
-#else
 // rms_exact with one correction: the f32 estimate of sqrt(S * (1/n)) taken with
 // the reciprocal scaled by (1 - 2^-18) (inv_b) lies in sqrt(S/n) * [1 - 2^-19 -
 // 2^-22, 1 - 2^-19 + 2^-22] (rcp, product and sqrt each within a few ulp), so
@@ -433,7 +259,9 @@ __global__ void __launch_bounds__(256, MM_RMS_MINB) comp_rms_kernel(CompArgs a) 
 #pragma unroll
         for (int j = 0; j < B; ++j)
             if (whole || j < pn) {
+#ifndef MM_RMS_NOSTORE  // (ablation builds: timing only)
                 Mo[e + (uint32_t)j * GS32] = mq[j];
+#endif
                 const double d = div_cr(mq[j], Rf, rR);
                 ce = vmax(mq[j], ce - d);
                 De += d;
@@ -453,7 +281,12 @@ __global__ void __launch_bounds__(256, MM_RMS_MINB) comp_rms_kernel(CompArgs a) 
             for (int j = 0; j < B; ++j) r[j] = j < nv ? rms_step(buf[k][j], st) : 0u;
             double m[B];
 #pragma unroll
-            for (int j = 0; j < B; ++j) m[j] = lut[r[j]];
+            for (int j = 0; j < B; ++j)
+#ifdef MM_RMS_NOGATHER  // (ablation builds: timing only)
+                m[j] = (double)r[j];
+#else
+                m[j] = lut[r[j]];
+#endif
             __builtin_amdgcn_sched_barrier(0);
             if (q > 0) flush(true);
 #pragma unroll
@@ -479,9 +312,18 @@ __global__ void __launch_bounds__(256, MM_RMS_MINB) comp_rms_kernel(CompArgs a) 
         }
         flush(false);
     };
-    if (steady) run(BoolTag<true>{}, ld_steady, T);
-    else if (len > 0) run(BoolTag<false>{}, ld, len);
-    for (int i = max(len, 0); i < a.TP; ++i, e += GS32) Mo[e] = 0.0;
+    // A tile whose largest possible window sum (S at its start plus every frame that
+    // enters during it; drops only lower it) stays below n r0^2 has no active frame
+    // (r >= r0 iff n r0^2 <= S; integers below 2^53 in f64): its M rows are all 0,
+    // and no kernel reads them (comp_describe and the solve walk active tiles only,
+    // comp_apply takes M = 0 for a tile without active frames), so it loads,
+    // gathers and stores nothing.  (n is fixed once the window is full.)
+    const bool quiet = skip == 0 && (double)n * ((double)r0 * (double)r0) > S + a.E[b][g];
+    if (!quiet) {
+        if (steady) run(BoolTag<true>{}, ld_steady, T);
+        else if (len > 0) run(BoolTag<false>{}, ld, len);
+        for (int i = max(len, 0); i < a.TP; ++i, e += GS32) Mo[e] = 0.0;
+    }
     a.cnt[b][g] = active;
     a.mmax[b][g] = lut[rmx];
     {  // active tiles of the column block (the wave's tiles share it)
@@ -499,8 +341,210 @@ __global__ void __launch_bounds__(256, MM_RMS_MINB) comp_rms_kernel(CompArgs a) 
         atomicAdd(a.total[b] + c, active);
     }
 }
-#endif
 
+
+// ---- comp_rms with the table gathers and M stores transposed through LDS -------
+// (TPS == 4: a workgroup = one column block = 256 consecutive tiles of a chunk.)
+// The per-frame rms runs as in comp_rms (lane = tile, coalesced band rows); per
+// block of RMS_B frames three phases exchange through LDS:
+//   A  lane = tile: the exact rms r of RMS_B frames -> R[j][tile];
+//   B  each wave gathers M = lut[r] for its own 64 tiles x RMS_B frames with lanes
+//      over (8 tiles x 8 CONSECUTIVE frames): a lane group of one tile reads
+//      nearly the same r, so a gather touches ~8 table lines instead of 64 (the
+//      round-5 profile had comp_rms TA-bound: L1 address stalls 55 % of its time);
+//   C  lane = column, wave = tile position: M rows of 64 consecutive columns are
+//      stored as one 512-byte run, and the lane keeps its tile's (max,+) release
+//      summary (frames in order).
+// Gathers of block q are in flight while block q+1's rms runs; one workgroup
+// barrier per block (double-buffered R and M stages).
+constexpr int RT_SLOTS = 4 * 68;                      // M stage slots: position-major, 68 per position
+constexpr int RT_RPAD = 264, RT_MPAD = 296;           // row strides (words / doubles), bank spread
+__device__ __forceinline__ int rt_slot(int tl) { return (tl & 3) * 68 + (tl >> 2); }
+
+__global__ void __launch_bounds__(256, MM_RMS_MINB) comp_rms_t_kernel(CompArgs a) {
+    __shared__ uint16_t Rs[2][RMS_B][RT_RPAD];
+    __shared__ double Mst[2][RMS_B][RT_MPAD];
+    const int b = blockIdx.y;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t cbk = blockIdx.x;                   // global column block
+    const int64_t cc = (cbk * 64) / a.SPC;
+    const int64_t jt0 = (cbk * 64 - cc * a.SPC) * 4;  // its first tile in the chunk
+    const short2 *x = a.band[b];
+    const int look = a.look[b], T = a.T, ch = a.ch;
+    const uint32_t G = (uint32_t)a.G;
+    const uint32_t r0 = a.r0[b];
+    const double *lut = a.lut[b];
+    const double Rf = a.release_frames[b], rR = a.rcp_release[b];
+    const int64_t chunk0 = cc * a.K * T;
+    // ---- phase A role: tile tlA = 64 w + lane of the block
+    const int tlA = w * 64 + lane;
+    const int64_t jtA = jt0 + tlA, gA = cc * a.K + jtA;
+    const bool vA = jtA < a.K && gA < a.G;
+    // invalid lanes (past the chunk's tiles or the track: a wave's LAST lanes, so lane 0
+    // is valid whenever any lane is) load as lane 0 does: in bounds, never used
+    const uint32_t g32 = vA ? (uint32_t)gA : (uint32_t)__builtin_amdgcn_readfirstlane((int)gA);
+    const int64_t f0 = (int64_t)g32 * T;
+    const int lenA = vA ? (int)min((int64_t)T, a.N_proc - f0) : 0;
+    const int64_t lo0 = max(chunk0, f0 - look);
+    double S = 0.0;
+    if (vA) {
+        const int kf = look / T;
+        for (int t = 1; t <= kf; ++t)
+            if (((int64_t)g32 - t) * T >= chunk0) S += a.E[b][g32 - t];
+        if (look % T != 0 && ((int64_t)g32 - kf - 1) * T >= chunk0) S += a.tail[b][g32 - kf - 1];
+    }
+    const int64_t d_first = max(f0 - look, chunk0);
+    const int skip = vA ? (int)(d_first - (f0 - look)) : 0;
+    const uint32_t gd = (uint32_t)(d_first / T);
+    const int nd = (int)(d_first - (int64_t)gd * T);
+    double n = (double)((f0 - lo0) * ch);
+    float inv = n > 0.0 ? rcp_biased(n) : 0.f;
+    int i_proc = 0, active = 0;
+    uint32_t rmx = 0;
+    struct Pair {
+        short2 in, drop;
+    };
+    const bool steady = __all(!vA || (skip == 0 && lenA == T)) && look > 0;
+    const int64_t dgo = (int64_t)__builtin_amdgcn_readfirstlane((int)((int64_t)gd - (int64_t)g32));
+    const int nd_u = __builtin_amdgcn_readfirstlane(nd);
+    auto ld_steady = [&](int i) __attribute__((always_inline)) {
+        i = min(i, T - 1);
+        Pair p;
+        p.in = (x + (int64_t)i * G)[g32];
+        int k = nd_u + i;
+        const int wrap = k >= T ? 1 : 0;
+        k -= wrap * T;
+        p.drop = (x + (int64_t)k * G + dgo + wrap)[g32];
+        return p;
+    };
+    auto ld = [&](int i) __attribute__((always_inline)) {
+        i = max(min(i, lenA - 1), 0);
+        Pair p;
+        p.in = x[(uint32_t)i * G + g32];
+        int k = nd + max(i - skip, 0);
+        const int wrap = k >= T ? 1 : 0;
+        k -= wrap * T;
+        p.drop = x[(uint32_t)k * G + gd + (uint32_t)wrap];
+        return p;
+    };
+    auto rms_step = [&](Pair p, auto st) __attribute__((always_inline)) {
+        uint32_t r;
+        if constexpr (decltype(st)::value) {
+            r = rms_exact1(S, n, inv);
+            S += (double)frame_energy2(p.in) - (double)frame_energy2(p.drop);
+        } else {
+            r = n > 0.0 ? rms_exact1(S, n, inv) : 0u;
+            const bool drops = i_proc >= skip;
+            S += (double)frame_energy2(p.in) - (drops ? (double)frame_energy2(p.drop) : 0.0);
+            if (!drops) {
+                n += ch;
+                inv = rcp_biased(n);
+            }
+            ++i_proc;
+        }
+        active += r >= r0 ? 1 : 0;
+        rmx = max(rmx, r);
+        return r;
+    };
+    // ---- phase B role: lanes over (8 tiles x 8 frames) of the wave's own tiles
+    const int jB = lane & 7;                          // frame in the block
+    // ---- phase C role: column lane of the block, tile position w
+    const int tlC = lane * 4 + w;
+    const int64_t jtC = jt0 + tlC, gC = cc * a.K + jtC;
+    const bool vC = jtC < a.K && gC < a.G;
+    const int lenC = vC ? (int)min((int64_t)T, a.N_proc - gC * T) : 0;
+    double *Mo = chunk_plane(a, b, cc);
+    uint32_t eC = col_elem(a, cc * a.SPC + jtC / 4) + (uint32_t)(w * a.TP) * 64u;  // row w*TP of its column
+    double ce = 0.0, De = 0.0;
+    const int slotC = w * 68 + lane;                  // == rt_slot(tlC)
+
+    constexpr int B = RMS_B, NB = MM_RMS_NB;
+    const int NBK = (T + B - 1) / B;
+    Pair buf[NB][B];
+    double gm[B];                                     // phase B gathers in flight
+    auto issue_gathers = [&](int q) __attribute__((always_inline)) {
+        asm volatile("" ::: "memory");                // (R written by this wave above: keep the reads after)
+#pragma unroll
+        for (int r8 = 0; r8 < B; ++r8) {
+            const int tl = w * 64 + r8 * 8 + (lane >> 3);
+            gm[r8] = lut[Rs[q & 1][jB][tl]];
+        }
+    };
+    auto finish_gathers = [&](int q) __attribute__((always_inline)) {
+#pragma unroll
+        for (int r8 = 0; r8 < B; ++r8) {
+            const int tl = w * 64 + r8 * 8 + (lane >> 3);
+            Mst[q & 1][jB][rt_slot(tl)] = gm[r8];
+        }
+    };
+    auto phase_c = [&](int q) __attribute__((always_inline)) {
+        const int nv = min(B, T - q * B);             // uniform
+#pragma unroll
+        for (int j = 0; j < B; ++j) {
+            if (j < nv) {
+                const double m = Mst[q & 1][j][slotC];
+                if (vC) Mo[eC] = m;
+                eC += 64u;
+                const double d = div_cr(m, Rf, rR);
+                ce = vmax(m, ce - d);
+                De += d;
+            }
+        }
+    };
+    auto run = [&](auto st, auto &&load) __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+#pragma unroll
+            for (int j = 0; j < B; ++j) buf[k][j] = load(k * B + j);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        auto body = [&](int k, int q) __attribute__((always_inline)) {
+            // A: rms of block q (frames past the lane's tile: r = 0, M = 0)
+            uint32_t r[B];
+            const int nvA = lenA - q * B;             // (uniform when steady)
+#pragma unroll
+            for (int j = 0; j < B; ++j) r[j] = j < nvA ? rms_step(buf[k][j], st) : 0u;
+#pragma unroll
+            for (int j = 0; j < B; ++j) buf[k][j] = load((q + NB) * B + j);
+#pragma unroll
+            for (int j = 0; j < B; ++j) Rs[q & 1][j][tlA] = (uint16_t)r[j];
+            if (q > 0) finish_gathers(q - 1);
+            issue_gathers(q);
+            __syncthreads();
+            if (q > 0) phase_c(q - 1);
+        };
+        for (int q0 = 0; q0 < NBK; q0 += NB) {
+#pragma unroll
+            for (int k = 0; k < NB; ++k)
+                if (q0 + k < NBK) body(k, q0 + k);
+        }
+    };
+    // (a wave's invalid tiles are its last lanes: lane 0 is valid iff any lane is, so
+    // the readfirstlane values above are a valid lane's; a wave past the chunk's tiles
+    // loads nothing)
+    if (!__any(vA)) run(BoolTag<true>{}, [](int) { return Pair{make_short2(0, 0), make_short2(0, 0)}; });
+    else if (steady) run(BoolTag<true>{}, ld_steady);
+    else run(BoolTag<false>{}, ld);
+    finish_gathers(NBK - 1);
+    __syncthreads();
+    phase_c(NBK - 1);
+    // rows past the tile's frames (the padding to TP) hold M = 0 (identity steps)
+    if (vC)
+        for (int i = T; i < a.TP; ++i, eC += 64u) Mo[eC] = 0.0;
+    if (vC) reinterpret_cast<double2 *>(a.ced[b])[gC] = make_double2(ce, De);
+    (void)lenC;
+    if (vA) {
+        a.cnt[b][gA] = active;
+        a.mmax[b][gA] = lut[rmx];
+    }
+    {  // active tiles of the column block
+        const int na = (int)__popcll(__ballot(vA && active != 0));
+        if (lane == 0 && na) atomicAdd(a.cbtot[b] + cbk, na);
+    }
+    int v = vA ? active : 0;  // per-chunk active count (statistics)
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (lane == 0 && v) atomicAdd(a.total[b] + cc, v);
+}
 
 struct BandStep {
     double A, R, rA, rR;
@@ -1465,10 +1509,13 @@ __global__ void __launch_bounds__(192, MM_APPLY_MINB) comp_apply_kernel(CompArgs
     const double *Ml = Mp + e0;      // this lane's column, its tile's row 0
     // rows past the tile's frames hold M = 0 (comp_rms): identity steps whose
     // output is unused; samples are clamped to the tile
+    // a tile without active frames has M = 0 throughout: comp_rms may not have
+    // stored its rows (quiet tiles), so it takes 0 instead of loading them
+    const bool act = valid && a.cnt[b][g] != 0;
     auto load = [&](int n0, double (&m)[S], short2 (&v)[S], bool with_m) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < S; ++j) {
-            if (with_m) m[j] = Ml[(size_t)min(n0 + j, T - 1) * GS32];  // (uniform row)
+            if (with_m) m[j] = act ? Ml[(size_t)min(n0 + j, T - 1) * GS32] : 0.0;  // (uniform row)
             v[j] = Xl[(size_t)min((uint32_t)(n0 + j), last) * G32];
         }
     };

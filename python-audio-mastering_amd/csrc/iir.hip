@@ -114,16 +114,6 @@ __device__ __forceinline__ double df2t(double x, double &z0, double &z1, const d
 #ifndef MM_KW_NB
 #define MM_KW_NB 3
 #endif
-#ifndef MM_P1_UNROLL
-#define MM_P1_UNROLL 4
-#endif
-#ifndef MM_P1_DOT
-#define MM_P1_DOT 0
-#endif
-// pass 1 of the full-tile paths as the dot product with the zero-state response
-// (lookback.h resp_row) instead of the cascade
-constexpr bool P1_DOT = MM_P1_DOT != 0;
-constexpr int P1_UNROLL = MM_P1_UNROLL;
 constexpr int EQ_STAGE = MM_EQ_STAGE;  // frames per tile staged through LDS per step
 
 struct EqArgs {
@@ -261,92 +251,6 @@ __device__ void eq_pass2(const EqArgs &a, int64_t g, int c, int len, double (&z)
 // loops carry no per-lane exit, and the exciter / width switches are template
 // arguments instead of per-frame tests.
 
-// pass 1 from the LDS-staged input: exciter -> the f32 scratch a.xs (tile-major,
-// read back by pass 2) -> the zero-state cascade (fused: it only feeds the carry)
-template <int NS, int CH, bool I16, bool SAT, bool DOT>
-__device__ void eq_pass1_full(const EqArgs &a, const double *resp, int64_t g0, int t, int c, double (&z)[NS][2],
-                              float *stage) {
-    constexpr int TPB = LB_THREADS / CH;
-    constexpr int ROW = (EQ_STAGE + 1) * CH;
-    constexpr int ITEMS = TPB * EQ_STAGE / LB_THREADS;
-    const int T = a.T;
-    const int nsteps = (T + EQ_STAGE - 1) / EQ_STAGE;
-    const uint32_t tid = threadIdx.x;  // (unsigned: scalar row base + 32-bit lane offset)
-    const double(*sos)[5] = a.sos;
-    const int64_t GC = a.G * CH;          // floats per scratch row
-    float *xs0 = a.xs + g0 * CH;          // the block's first element of row 0 (uniform)
-    float regs[ITEMS][CH];
-    auto load = [&](int step) {
-#pragma unroll
-        for (int r = 0; r < ITEMS; ++r) {
-            const int idx = tid + r * LB_THREADS;
-            const int tt = idx / EQ_STAGE, j = idx % EQ_STAGE;
-            const int n = step * EQ_STAGE + j;
-            const int64_t f = (g0 + tt) * T + n;
-            const bool ok = n < T && f < a.N_in;
-            const int64_t fc = ok ? f : 0;
-            if constexpr (I16) {
-                if constexpr (CH == 2) {
-                    const short2 v = *reinterpret_cast<const short2 *>(a.in16 + 2 * fc);
-                    regs[r][0] = ok ? (float)v.x * (1.0f / 32768.0f) : 0.f;
-                    regs[r][1] = ok ? (float)v.y * (1.0f / 32768.0f) : 0.f;
-                } else {
-                    regs[r][0] = ok ? (float)a.in16[fc] * (1.0f / 32768.0f) : 0.f;
-                }
-            } else if constexpr (CH == 2) {
-                const float2 v = *reinterpret_cast<const float2 *>(a.in + 2 * fc);
-                regs[r][0] = ok ? v.x : 0.f;
-                regs[r][1] = ok ? v.y : 0.f;
-            } else {
-                const float v = a.in[fc];
-                regs[r][0] = ok ? v : 0.f;
-            }
-        }
-    };
-    auto store = [&](int buf) {
-#pragma unroll
-        for (int r = 0; r < ITEMS; ++r) {
-            const int idx = tid + r * LB_THREADS;
-            const int tt = idx / EQ_STAGE, j = idx % EQ_STAGE;
-            float *dst = stage + buf * TPB * ROW + tt * ROW + j * CH;
-#pragma unroll
-            for (int q = 0; q < CH; ++q) dst[q] = regs[r][q];
-        }
-    };
-    load(0);
-    store(0);
-    lds_barrier();
-    for (int step = 0; step < nsteps; ++step) {
-        const int cur = step & 1;
-        if (step + 1 < nsteps) load(step + 1);
-        const float *row = stage + cur * TPB * ROW + t * ROW + c;
-        const int nj = min(EQ_STAGE, T - step * EQ_STAGE);  // uniform
-        float *xr = xs0 + (int64_t)(step * EQ_STAGE) * GC;
-#pragma unroll P1_UNROLL
-        for (int j = 0; j < nj; ++j) {
-            float x = row[j * CH];
-            if constexpr (SAT) x = saturate(x, a.sat);
-            (xr + (int64_t)j * GC)[tid] = x;
-            if constexpr (DOT) {  // z += h[T-1-n] x_n: 2NS independent FMAs, no cascade chain
-                double h[2 * NS];
-                resp_row(resp, step * EQ_STAGE + j, h);
-                const double y = (double)x;
-#pragma unroll
-                for (int s = 0; s < NS; ++s) {
-                    z[s][0] = fma(h[2 * s], y, z[s][0]);
-                    z[s][1] = fma(h[2 * s + 1], y, z[s][1]);
-                }
-            } else {
-                double y = (double)x;
-#pragma unroll
-                for (int s = 0; s < NS; ++s) y = df2t<false>(y, z[s][0], z[s][1], sos[s]);
-            }
-        }
-        if (step + 1 < nsteps) store(cur ^ 1);
-        lds_barrier();
-    }
-}
-
 // pass 2 from the scratch: EQ (scipy order) -> width -> int16, all rows uniform
 template <int NS, int CH, bool WIDTH>
 __device__ void eq_pass2_full(const EqArgs &a, int64_t g0, double (&z)[NS][2]) {
@@ -396,18 +300,12 @@ __global__ void __launch_bounds__(LB_THREADS, 4) eq_kernel(EqArgs a, LbArgs lb, 
     double zs[NS][2];
 #pragma unroll
     for (int s = 0; s < NS; ++s) zs[s][0] = zs[s][1] = 0.0;
-    // block-uniform: every tile of the block is whole (all blocks but the track's last)
-    const bool full = (g0 + TPB) * a.T <= a.N_proc && (!P1_DOT || lb.resp);
-#ifdef MM_EQ_P1_GENERIC  // (ablation builds)
-    if (false) {
-#else
-    if (full) {
-#endif
-        if (a.sat.on) eq_pass1_full<NS, CH, I16, true, P1_DOT>(a, lb.resp, g0, t, c, zs, stage);
-        else eq_pass1_full<NS, CH, I16, false, P1_DOT>(a, lb.resp, g0, t, c, zs, stage);
-    } else {
-        eq_pass<NS, CH, false, I16>(a, g0, t, c, len, zs, stage);
-    }
+    // block-uniform: every tile of the block is whole (all blocks but the track's last).
+    // Pass 1 stays the general LDS-staged loop at every block (a uniform-row variant
+    // with the exciter switch as a template argument measured slower: eq 0.152 ->
+    // 0.166 ms); pass 2 takes the uniform-row path on full blocks.
+    const bool full = (g0 + TPB) * a.T <= a.N_proc;
+    eq_pass<NS, CH, false, I16>(a, g0, t, c, len, zs, stage);
     double z[DIM], s[DIM], rst[DIM];
 #pragma unroll
     for (int s_ = 0; s_ < NS; ++s_) {
@@ -549,8 +447,7 @@ __device__ __forceinline__ void xo_pass(const XoArgs &a, int64_t g, int c, int l
 // alike); the tail sums take the frames n >= tail_from through a select on the
 // uniform frame index.
 template <int CH, bool P2>
-__device__ __forceinline__ void xo_pass_full(const XoArgs &a, const double *resp, int64_t g0, int tid,
-                                             double (&z)[4][2]) {
+__device__ __forceinline__ void xo_pass_full(const XoArgs &a, int64_t g0, int tid, double (&z)[4][2]) {
     const double(*sos)[5] = a.sos;
     const int T = a.T;
     const int64_t G2 = a.G * 2;
@@ -564,17 +461,6 @@ __device__ __forceinline__ void xo_pass_full(const XoArgs &a, const double *resp
         T, [&](int i) { return (qin0 + (int64_t)min(i, T - 1) * G2)[lo]; },
         [&](int16_t q) {
             const double x = (double)(int32_t)q * (1.0 / 32768.0);  // AME:199 int16 -> f32, exact
-            if (!P2 && P1_DOT) {  // z += h[T-1-n] x_n (lb_resp rows): 8 independent FMAs
-                double h[8];
-                resp_row(resp, pn, h);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    z[k][0] = fma(h[2 * k], x, z[k][0]);
-                    z[k][1] = fma(h[2 * k + 1], x, z[k][1]);
-                }
-                ++pn;
-                return;
-            }
             double yl = df2t<P2>(x, z[0][0], z[0][1], sos[0]);
             yl = df2t<P2>(yl, z[1][0], z[1][1], sos[1]);
             double yh = df2t<P2>(x, z[2][0], z[2][1], sos[2]);
@@ -629,8 +515,8 @@ __global__ void __launch_bounds__(LB_THREADS, 4) xover_kernel(XoArgs a, LbArgs l
     const int len = valid ? (int)min((int64_t)a.T, a.N_proc - g * a.T) : 0;
     double zs[4][2] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
     const int64_t g0 = (int64_t)blk * TPB;
-    const bool full = (g0 + TPB) * a.T <= a.N_proc && (!P1_DOT || lb.resp);  // block-uniform
-    if (full) xo_pass_full<CH, false>(a, lb.resp, g0, tid, zs);
+    const bool full = (g0 + TPB) * a.T <= a.N_proc;  // block-uniform
+    if (full) xo_pass_full<CH, false>(a, g0, tid, zs);
     else if (valid) xo_pass<CH, false>(a, g, c, len, zs);
     double z[8], s[8], rst[8];
 #pragma unroll
@@ -645,7 +531,7 @@ __global__ void __launch_bounds__(LB_THREADS, 4) xover_kernel(XoArgs a, LbArgs l
         zs[k][0] = s[2 * k];
         zs[k][1] = s[2 * k + 1];
     }
-    if (full) xo_pass_full<CH, true>(a, lb.resp, g0, tid, zs);
+    if (full) xo_pass_full<CH, true>(a, g0, tid, zs);
     else if (valid) xo_pass<CH, true>(a, g, c, len, zs);
 }
 

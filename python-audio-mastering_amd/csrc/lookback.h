@@ -47,19 +47,7 @@ struct LbArgs {
     unsigned *error;        // [1]      set to 1 on a spin timeout
     const double *init;     // [CH][8]  state at the track start (or null = 0)
     int64_t line_tiles;     // line starts at tiles g % line_tiles == 0
-    const double *resp;     // [T][8] zero-state response rows (mastering.hip response_table) or null
 };
-
-// Row n of the response table in SGPRs: a wave-uniform load through the constant
-// address space is a scalar (s_load) load, so the dot-product pass keeps its
-// coefficients out of VGPRs and off the vector memory queue.
-typedef __attribute__((address_space(4))) const double cdouble_t;
-template <int DIM>
-__device__ __forceinline__ void resp_row(const double *resp, int n, double (&h)[DIM]) {
-    const cdouble_t *p = (const cdouble_t *)(resp + (int64_t)n * 8);
-#pragma unroll
-    for (int d = 0; d < DIM; ++d) h[d] = p[d];
-}
 
 typedef __attribute__((address_space(1))) unsigned gu32;
 typedef __attribute__((address_space(1))) unsigned long long gu64;

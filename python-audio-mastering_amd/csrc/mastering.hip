@@ -189,38 +189,11 @@ static inline unsigned blocks_for(int64_t n, int t) { return (unsigned)((n + t -
 
 // ------------------------------------------------------- look-back plumbing
 // Transition tables of one filter stage (uploaded only when they change).
-// Zero-state response of a stage's cascade (lookback.h lb_resp): rows n = 0..T-1
-// hold h[T-1-n], h[k] the state k frames after a unit impulse (state index 2s+i =
-// z_i of section s; sections [0, nb0) one cascade, the rest a second one fed by the
-// same input), run in x87 long double and rounded once, so the tile's zero-state
-// end state is sum_n row[n] * x_n.
-static void response_table(const mm_iir &f, int T, double *out) {
-    const int ns = f.nsec, nb0 = (f.nsec_branch0 > 0 && f.nsec_branch0 < ns) ? f.nsec_branch0 : ns;
-    long double z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int k = 0; k < T; ++k) {
-        const long double x = k == 0 ? 1.0L : 0.0L;
-        long double xin = x;
-        for (int s = 0; s < ns; ++s) {
-            if (s == nb0) xin = x;  // the second cascade restarts from the input
-            const double *c = f.sos[s];
-            const long double y = (long double)c[0] * xin + z[2 * s];
-            z[2 * s] = (long double)c[1] * xin - (long double)c[3] * y + z[2 * s + 1];
-            z[2 * s + 1] = (long double)c[2] * xin - (long double)c[4] * y;
-            xin = y;
-        }
-        double *row = out + (size_t)(T - 1 - k) * 8;
-        for (int d = 0; d < 8; ++d) row[d] = d < 2 * ns ? (double)z[d] : 0.0;
-    }
-}
-
 static int upload_tables(mm_ctx *c, const char *name, const mm_iir &f, LbArgs &lb) {
-    const size_t nm = (size_t)(MM_TILE_POW + MM_BLK_POW) * 64;
-    const bool resp = f.tile >= 1 && f.tile <= 512 && std::strcmp(name, "kweight") != 0;
-    const size_t n = nm + (resp ? (size_t)f.tile * 8 : 0);
+    const size_t n = (size_t)(MM_TILE_POW + MM_BLK_POW) * 64;
     std::vector<double> host(n);
     memcpy(host.data(), f.phi_tile_pow, sizeof f.phi_tile_pow);
     memcpy(host.data() + MM_TILE_POW * 64, f.phi_blk_pow, sizeof f.phi_blk_pow);
-    if (resp) response_table(f, f.tile, host.data() + nm);
     const std::string key = std::string("tab_") + name;
     double *d;
     RET(get_buf(c, key.c_str(), n, &d));
@@ -232,7 +205,6 @@ static int upload_tables(mm_ctx *c, const char *name, const mm_iir &f, LbArgs &l
     }
     lb.pw_tile = d;
     lb.pw_blk = d + MM_TILE_POW * 64;
-    lb.resp = resp ? d + nm : nullptr;
     return MM_OK;
 }
 
@@ -608,7 +580,10 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
         ca.se0[b] = ca.sjump ? se0s + (size_t)b * NS : nullptr;
         ca.cbtot[b] = reinterpret_cast<int32_t *>(claims + (size_t)3 * NS) + (size_t)b * (NS / 64);
     }
-    RET(launch(c, "comp_rms", comp_rms_kernel, dim3(blocks_for(NS / 64 * ca.TPS, 4), 3), dim3(256), 0, ca));
+    if (ca.TPS == 4 && !getenv("MM_RMS_V2"))  // column block = one workgroup: gathers / stores through LDS
+        RET(launch(c, "comp_rms", comp_rms_t_kernel, dim3((unsigned)(NS / 64), 3), dim3(256), 0, ca));
+    else
+        RET(launch(c, "comp_rms", comp_rms_kernel, dim3(blocks_for(NS / 64 * ca.TPS, 4), 3), dim3(256), 0, ca));
     RET(launch(c, "comp_describe", comp_describe_kernel, dim3((unsigned)(NS / 64), 3), dim3(64 * ca.TPS), 0, ca));
     RET(launch(c, "comp_pass0", comp_pass0_kernel, dim3(blocks_for(NS, PASS0_BLOCK), 3), dim3(PASS0_BLOCK), 0, ca));
     c->comp_on = true;
