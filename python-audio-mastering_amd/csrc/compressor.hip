@@ -467,7 +467,11 @@ __global__ void __launch_bounds__(256, MM_RMS_MINB) comp_rms_t_kernel(CompArgs a
 #pragma unroll
         for (int r8 = 0; r8 < B; ++r8) {
             const int tl = w * 64 + r8 * 8 + (lane >> 3);
+#ifdef MM_RMS_NOGATHER  // (ablation builds: timing only)
+            gm[r8] = (double)Rs[q & 1][jB][tl];
+#else
             gm[r8] = lut[Rs[q & 1][jB][tl]];
+#endif
         }
     };
     auto finish_gathers = [&](int q) __attribute__((always_inline)) {
@@ -483,7 +487,9 @@ __global__ void __launch_bounds__(256, MM_RMS_MINB) comp_rms_t_kernel(CompArgs a
         for (int j = 0; j < B; ++j) {
             if (j < nv) {
                 const double m = Mst[q & 1][j][slotC];
+#ifndef MM_RMS_NOSTORE  // (ablation builds: timing only)
                 if (vC) Mo[eC] = m;
+#endif
                 eC += 64u;
                 const double d = div_cr(m, Rf, rR);
                 ce = vmax(m, ce - d);

@@ -73,14 +73,44 @@ __global__ void __launch_bounds__(GATE_THREADS) gate_kernel(GateArgs a) {
     double zc[GATE_CACHE], lc[GATE_CACHE];  // the thread's first blocks (a 5-min track: 3 each)
     double sum = 0.0;
     long long cnt = 0;
-    int i = 0;
-    for (int64_t j = j0 + t; j < j1; j += GATE_THREADS, ++i) {
+    // the cached blocks first, their segment loads issued together (one latency
+    // instead of a dependent chain per block: the kernel is a single workgroup)
+    int32_t b0[GATE_CACHE], b1[GATE_CACHE];
+#pragma unroll
+    for (int k = 0; k < GATE_CACHE; ++k) {
+        const int64_t j = j0 + t + (int64_t)k * GATE_THREADS;
+        b0[k] = j < j1 ? a.blk_s0[j] : 0;
+        b1[k] = j < j1 ? a.blk_s1[j] : 0;
+    }
+    // (a 0.4 s block spans 4 segments of 0.1 s, 5 at a ragged end: the first four
+    // loads of every block are issued without a wait)
+    double sv[GATE_CACHE][4];
+#pragma unroll
+    for (int k = 0; k < GATE_CACHE; ++k)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) sv[k][u] = b0[k] + u < b1[k] ? a.seg[b0[k] + u] : 0.0;
+#pragma unroll
+    for (int k = 0; k < GATE_CACHE; ++k) {
+        double acc = 0.0;  // segment order, as gate_block_z
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (b0[k] + u < b1[k]) acc += sv[k][u];
+        for (int s_ = b0[k] + 4; s_ < b1[k]; ++s_) acc += a.seg[s_];
+        zc[k] = a.scale * acc;
+    }
+#pragma unroll
+    for (int k = 0; k < GATE_CACHE; ++k) {
+        const int64_t j = j0 + t + (int64_t)k * GATE_THREADS;
+        lc[k] = -0.691 + 10.0 * log10(zc[k]);
+        if (j < j1 && lc[k] >= -70.0) {
+            sum += zc[k];
+            ++cnt;
+        }
+    }
+    int i = GATE_CACHE;
+    for (int64_t j = j0 + t + (int64_t)GATE_CACHE * GATE_THREADS; j < j1; j += GATE_THREADS, ++i) {
         const double z = gate_block_z(a, j);
         const double l = -0.691 + 10.0 * log10(z);
-        if (i < GATE_CACHE) {
-            zc[i] = z;
-            lc[i] = l;
-        }
         if (l >= -70.0) {
             sum += z;
             ++cnt;

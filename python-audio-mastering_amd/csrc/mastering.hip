@@ -250,8 +250,9 @@ static int validate(mm_ctx *c, const mm_job *j) {
     if (j->lufs_on && j->kweight.tpb != LB_THREADS) return set_err(c, MM_ERR_ARG, "K-weighting tables built for %d tiles/block", j->kweight.tpb);
     if (j->eq.nsec > 0 && j->eq.tile != j->tile) return set_err(c, MM_ERR_ARG, "eq tables built for %d-frame tiles", j->eq.tile);
     if (j->multiband_on && j->xover.tile != j->tile) return set_err(c, MM_ERR_ARG, "crossover tables built for %d-frame tiles", j->xover.tile);
-    if (j->lufs_on && j->kweight.tile != j->tile)
-        return set_err(c, MM_ERR_ARG, "K-weighting tables built for %d-frame tiles", j->kweight.tile);
+    if (j->lufs_on && (j->kweight.tile < 1 || j->tile % j->kweight.tile != 0))
+        return set_err(c, MM_ERR_ARG, "K-weighting tables built for %d-frame (sub-)tiles, not a divisor of %d",
+                       j->kweight.tile, j->tile);
     if (j->multiband_on) {
         if (j->xover.nsec != 4 || j->xover.nsec_branch0 != 2) return set_err(c, MM_ERR_ARG, "crossover must be 2+2 sections");
         for (int b = 0; b < 3; ++b) {
@@ -622,7 +623,10 @@ static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
         nch = sg.chunks;
         spc = sg.cols_per_chunk;
     }
-    RET(setup_control(c, nblk, nch, 3 * nch * spc + 3 * nch * spc / 64));  // claim stamps, column-block counts
+    // (each look-back region also holds the K-weighting stage's blocks: sub-tile lanes)
+    const unsigned nblk_kw = j->lufs_on ? blocks_for(std::max<int64_t>(G, 1) * (T / std::max(1, j->kweight.tile)),
+                                                     LB_THREADS) : 0u;
+    RET(setup_control(c, std::max(nblk, nblk_kw), nch, 3 * nch * spc + 3 * nch * spc / 64));  // claim stamps, column-block counts
 
     EqArgs ea{};
     ea.in = j->in_kind == MM_IN_I16 ? nullptr : static_cast<const float *>(d_in);
@@ -735,15 +739,18 @@ static int upload_geometry(mm_ctx *c) {
 static int kweight_launch(mm_ctx *c, const double *carry_in_host, double *line_end, double **seg_out) {
     const mm_job *j = &c->job;
     const int64_t G = c->G;
+    // one lane per sub-tile of kweight.tile frames (design.kweight_sub), `sub` per tile
+    const int sub = j->tile / j->kweight.tile;
+    const int64_t GS = G * sub;
     double *part, *seg;
     int64_t *part_seg;
-    RET(get_buf(c, "kw_part", (size_t)std::max<int64_t>(G, 1) * 2, &part));
-    RET(get_buf(c, "kw_part_seg", (size_t)std::max<int64_t>(G, 1), &part_seg));
+    RET(get_buf(c, "kw_part", (size_t)std::max<int64_t>(GS, 1) * 2, &part));
+    RET(get_buf(c, "kw_part_seg", (size_t)std::max<int64_t>(GS, 1), &part_seg));
     RET(get_buf(c, "kw_seg", (size_t)j->n_segs, &seg));
     RET(upload_geometry(c));
     LbArgs lb{};
     RET(upload_tables(c, "kweight", j->kweight, lb));
-    const unsigned nblk = blocks_for(G, LB_THREADS);
+    const unsigned nblk = blocks_for(GS, LB_THREADS);
     RET(lb_prepare(c, nblk, 1, lb, 2));
     if (carry_in_host) {
         double *init;
@@ -754,10 +761,10 @@ static int kweight_launch(mm_ctx *c, const double *carry_in_host, double *line_e
     }
     KwArgs ka{};
     ka.N_proc = j->frames_proc;
-    ka.G = G;
-    ka.T = j->tile;
-    ka.Gt = G;  // one lane per mix tile (sub-tiles measured slower, iir.hip)
-    ka.sub = 1;
+    ka.G = GS;
+    ka.T = j->kweight.tile;
+    ka.Gt = G;
+    ka.sub = sub;
     ka.ch = j->channels;
     for (int s_ = 0; s_ < 2; ++s_)
         for (int k = 0; k < 5; ++k) ka.sos[s_][k] = j->kweight.sos[s_][k];
@@ -1042,21 +1049,23 @@ static int fused_geometry(mm_ctx *c, const mm_job *J, int n, FusedPlan *p) {
 // lg[2i] = L, lg[2i+1] = gain.
 static int fused_loudness(mm_ctx *c, const mm_job &j0, int n, const FusedPlan &p, double *lg) {
     const int64_t G = c->G;
+    const int sub = j0.tile / j0.kweight.tile;  // (design.kweight_sub)
+    const int64_t GS = G * sub;
     double *part, *seg;
     int64_t *part_seg;
-    RET(get_buf(c, "kw_part", (size_t)G * 2, &part));
-    RET(get_buf(c, "kw_part_seg", (size_t)G, &part_seg));
+    RET(get_buf(c, "kw_part", (size_t)GS * 2, &part));
+    RET(get_buf(c, "kw_part_seg", (size_t)GS, &part_seg));
     RET(get_buf(c, "kw_seg", (size_t)p.n_segs, &seg));
     LbArgs lb{};
     RET(upload_tables(c, "kweight", j0.kweight, lb));
-    const unsigned nblk = blocks_for(G, LB_THREADS);
+    const unsigned nblk = blocks_for(GS, LB_THREADS);
     RET(lb_prepare(c, nblk, 1, lb, 2));
     KwArgs ka{};
     ka.N_proc = p.P;
-    ka.G = G;
-    ka.T = j0.tile;
+    ka.G = GS;
+    ka.T = j0.kweight.tile;
     ka.Gt = G;
-    ka.sub = 1;
+    ka.sub = sub;
     ka.ch = j0.channels;
     for (int s_ = 0; s_ < 2; ++s_)
         for (int k = 0; k < 5; ++k) ka.sos[s_][k] = j0.kweight.sos[s_][k];

@@ -20,6 +20,7 @@ from __future__ import annotations
 import functools
 import hashlib
 import math
+import os
 
 import numpy as np
 import scipy.signal
@@ -86,6 +87,20 @@ def check_chunk_geometry(bounds, nominal: int, rate: int, multiband: bool):
             f = b - a
             if pydub_frame(pydub_len_ms(f, rate), rate) != f:
                 raise NotImplementedError(f"pydub overlay re-slicing changes a chunk's length at {rate} Hz")
+
+
+def kweight_sub(tile: int) -> int:
+    """K-weighting lanes per tile (the library takes any divisor of the tile as the
+    K-weighting tables' sub-tile).  1: the mono filter keeps one lane per tile — 3
+    sub-tiles of 75 frames (3x the lanes, 3x the look-back blocks) measured 0.083
+    against 0.066 ms on C2 (round 5; 25-frame sub-tiles 2x slower in round 2).
+    MM_KW_SUB sets it for A/B runs."""
+    env = os.environ.get("MM_KW_SUB")
+    if env:
+        sub = int(env)
+        if sub >= 1 and tile % sub == 0:
+            return sub
+    return 1
 
 
 def choose_tile(chunk_frames: int, preferred: int | None = None) -> int:

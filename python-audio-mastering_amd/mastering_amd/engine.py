@@ -124,7 +124,8 @@ class Job:
         j.comp_super = comp_super_frames(self.rate, self.tile)
         # --- loudness
         if lufs is not None:
-            self._fill_iir(j.kweight, design.kweight_sections(self.rate), [2], self.tile, design.LB_THREADS)
+            self._fill_iir(j.kweight, design.kweight_sections(self.rate), [2],
+                           self.tile // design.kweight_sub(self.tile), design.LB_THREADS)
             if seg_bounds is None:
                 nb, lo, hi, segb, scale = design.loudness_blocks(self.frames_proc, self.rate)
             else:  # rank-local segments; blocks are gated over the whole track elsewhere
