@@ -470,30 +470,10 @@ __device__ __forceinline__ void xo_pass_full(const XoArgs &a, int64_t g0, int ti
                 const int32_t qi[3] = {quantize_i32(yl), quantize_i32(ym), quantize_i32(yh)};
                 const int64_t ro = (int64_t)pn * G2;
                 int16_t *rows[3] = {b0 + ro, b1 + ro, b2 + ro};
-#ifdef MM_XO_PAIRSTORE
-                if constexpr (CH == 2) {
-                    // two stores per lane pair instead of three per lane: the even lane
-                    // writes band 0's (L, R), the odd lane band 1's, the even lane then
-                    // band 2's (fewer vector-memory operations in flight per frame)
-                    const int c = tid & 1;
-                    const int32_t o0 = pair_swap(qi[0]), o1 = pair_swap(qi[1]), o2 = pair_swap(qi[2]);
-                    const int32_t own = c == 0 ? qi[0] : qi[1], oth = c == 0 ? o0 : o1;
-                    const uint32_t lr = c == 0 ? ((uint32_t)(uint16_t)own | ((uint32_t)oth << 16))
-                                               : ((uint32_t)(uint16_t)oth | ((uint32_t)own << 16));
-                    reinterpret_cast<uint32_t *>(rows[c])[lo >> 1] = lr;
-                    if (c == 0)
-                        reinterpret_cast<uint32_t *>(rows[2])[lo >> 1] =
-                            (uint32_t)(uint16_t)qi[2] | ((uint32_t)o2 << 16);
-                }
-#endif
 #pragma unroll
                 for (int b = 0; b < 3; ++b) {
-#ifndef MM_XO_PAIRSTORE
                     if constexpr (CH == 2) rows[b][lo] = (int16_t)qi[b];
                     else reinterpret_cast<short2 *>(rows[b])[(uint32_t)tid] = make_short2((int16_t)qi[b], 0);
-#else
-                    if constexpr (CH != 2) reinterpret_cast<short2 *>(rows[b])[(uint32_t)tid] = make_short2((int16_t)qi[b], 0);
-#endif
                     const double e = (double)(uint32_t)(qi[b] * qi[b]);  // <= 2^30 (v_mul_i32_i24)
                     Ed[b] += e;
                     td[b] = fma(pn >= a.tail_from[b] ? 1.0 : 0.0, e, td[b]);
