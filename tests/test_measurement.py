@@ -15,7 +15,7 @@ import pytest  # noqa: E402
 WORKLOADS = ("C1", "C2", "C2hot", "C3", "C4", "C5")
 
 
-@pytest.mark.parametrize("w", ["C2", "C3", "C4", "C5"])
+@pytest.mark.parametrize("w", ["C1", "C2", "C2hot", "C3", "C4", "C5"])
 def test_profiles_match_sources(w):
     import bench
     path = os.path.join(ROOT, "profiles", f"{bench.PROFILE_ROUND}_{w}_pmc_summary.json")
@@ -54,8 +54,9 @@ def test_bench_lines_carry_the_contract_fields():
         assert abs(dk["algorithmic_bytes_per_launch"] * dk["launches_per_step"] - 16 * frames) <= 1e-6 * 16 * frames
         assert abs(dk["frac"] - dk["algorithmic_bytes_per_launch"] / (dk["avg_launch_ms"] / 1e3) / 1e9 / 8000.0) \
             <= 1e-9
-        if w != "C1":  # every multiband workload's line carries PMC traffic
-            assert r["traffic"] is not None, w
+        assert r["traffic"] is not None, w  # every line carries PMC traffic (C1 too since round 5)
+        v = r["valu"]  # the VALU floor beside the HBM one
+        assert v["lane_instr_per_frame"] > 0 and abs(v["frac"] - v["floor_ms"] / d["ms_per_step"]) < 1e-9, w
     with open(os.path.join(ROOT, "profiles", f"{bench.PROFILE_ROUND}_bench_C2.json")) as f:
         c2 = json.load(f)
     assert c2["roofline"]["traffic"] is not None and c2["cpu_baseline"]["cores"] >= 1

@@ -7,9 +7,10 @@
 #        per-kernel split; a variant is "ENV=x" (library env knob), "tune:NAME=V"
 #        (bench tune) or "lib:<path.so>" (an ablation build from tools/build_var.sh)
 #   bash tools/gpu.sh configs [C3 C4 C5 C1 ...]       bench lines of the other workloads
-#   bash tools/gpu.sh measure <round> [workloads...]  end-of-round measurement: tests, smoke,
+#   bash tools/gpu.sh measure <round> [notest] [workloads...]  end-of-round measurement: tests, smoke,
 #        per workload the rocprofv3 trace + PMC passes (tools/pmc.sh ->
 #        profiles/<round>_<w>_pmc_summary.json) and the bench line quoting them
+#   bash tools/gpu.sh lines <round> [workloads...]    the bench lines alone, quoting profiles/ as they are
 #   bash tools/gpu.sh firstcall                       first master_pcm on a fresh context
 #
 # Several modes may be chained in one call: bash tools/gpu.sh test -- iter -- configs C3
@@ -54,15 +55,29 @@ mode_configs() {
   for w in ${@:-C3 C5}; do bench_line $w - --workload $w || return 1; done
 }
 
-mode_measure() {
+mode_measure() {  # measure <round> [notest] [workloads...]
   local round=$1; shift
+  local skip_test=0; [ "$1" = "notest" ] && { skip_test=1; shift; }
   local wls="$@"; [ -z "$wls" ] && wls="C2 C2hot C3 C4 C5 C1"
-  mode_test || return 1
+  [ $skip_test -eq 1 ] || mode_test || return 1
   local w wl args cb
   for w in $wls; do
     case $w in C2hot) wl=C2; args="--params hot" ;; *) wl=$w; args="" ;; esac
     LABEL=${round}_$w bash tools/pmc.sh ${round}$w $wl $args || return 1
     cp profiles/${round}_${w}_* gpurun_out/profiles/
+    cb="--no-cpu-baseline"; case $w in C1|C2) cb="" ;; esac
+    timeout -k 10 400 python -u bench.py --workload $wl $args $cb > gpurun_out/bench_${round}_$w.json \
+      2> gpurun_out/bench_${round}_$w.err
+    local rc=$?; echo "bench $w rc=$rc"; [ $rc -ne 0 ] && { tail -20 gpurun_out/bench_${round}_$w.err; return $rc; }
+    python -c "import json; d=json.load(open('gpurun_out/bench_${round}_$w.json')); print('$w', round(d['value']/1e9,3), 'G frames/s', round(d['ms_per_step'],4), 'ms', 'traffic', d['roofline'].get('traffic'))"
+  done
+}
+
+mode_lines() {  # lines <round> [workloads...]: the bench lines alone (profiles already in profiles/)
+  local round=$1; shift
+  local w wl args cb
+  for w in ${@:-C2 C2hot C3 C4 C5 C1}; do
+    case $w in C2hot) wl=C2; args="--params hot" ;; *) wl=$w; args="" ;; esac
     cb="--no-cpu-baseline"; case $w in C1|C2) cb="" ;; esac
     timeout -k 10 400 python -u bench.py --workload $wl $args $cb > gpurun_out/bench_${round}_$w.json \
       2> gpurun_out/bench_${round}_$w.err

@@ -32,10 +32,15 @@ HBM_PEAK = 8.0e12
 VALU_PEAK = 256 * 4 * 2.4e9 / 4  # wave64 VALU instr/s: 1024 SIMDs, one f64 FMA per 4 cycles at 2.4 GHz
 
 
+# kernels whose launch name (the bench's per-kernel stats) differs from the function's
+ALIAS = {"comp_rms_t": "comp_rms"}
+
+
 def label(name):
     n = name.replace("void ", "").split("(")[0].split("<")[0]
     n = n.replace("mm::", "")
-    return n[: -len("_kernel")] if n.endswith("_kernel") else n
+    n = n[: -len("_kernel")] if n.endswith("_kernel") else n
+    return ALIAS.get(n, n)
 
 
 def counters(d, sub):
