@@ -460,8 +460,11 @@ __global__ void __launch_bounds__(256, MM_RMS_MINB) comp_rms_t_kernel(CompArgs a
 
     constexpr int B = RMS_B, NB = MM_RMS_NB;
     const int NBK = (T + B - 1) / B;
+    const int NBKP = (NBK + NB - 1) / NB * NB;        // blocks run (a multiple of NB; past NBK: empty)
     Pair buf[NB][B];
     double gm[B];                                     // phase B gathers in flight
+#pragma unroll
+    for (int j = 0; j < B; ++j) gm[j] = 0.0;
     auto issue_gathers = [&](int q) __attribute__((always_inline)) {
         asm volatile("" ::: "memory");                // (R written by this wave above: keep the reads after)
 #pragma unroll
@@ -481,20 +484,34 @@ __global__ void __launch_bounds__(256, MM_RMS_MINB) comp_rms_t_kernel(CompArgs a
             Mst[q & 1][jB][rt_slot(tl)] = gm[r8];
         }
     };
+    // Phase C's stores are unconditional buffer stores (an invalid lane or a row past
+    // the tile gets an offset past the plane: the store is dropped), so the compiler
+    // counts them exactly: with exec-masked stores its gather waits also waited for
+    // the previous block's stores (vmcnt is in order).  Measured neutral (0.203 ms
+    // either way: the kernel is bound by its L1 -> L2 request rate).
+    const __amdgpu_buffer_rsrc_t Mr =
+        __builtin_amdgcn_make_buffer_rsrc(Mo, (short)0, (int)(a.chunk_elems * 8), 0x00020000);
+    constexpr uint32_t DROP = 0xFFFFFFF0u;            // >= the plane's bytes (offsets fit 32 bits)
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
     auto phase_c = [&](int q) __attribute__((always_inline)) {
-        const int nv = min(B, T - q * B);             // uniform
+        const int nv = q >= 0 ? max(min(B, T - q * B), 0) : 0;  // uniform (q = -1, past the tile: none)
+        double m[B];
+#pragma unroll
+        for (int j = 0; j < B; ++j) m[j] = Mst[q & 1][j][slotC];
 #pragma unroll
         for (int j = 0; j < B; ++j) {
-            if (j < nv) {
-                const double m = Mst[q & 1][j][slotC];
 #ifndef MM_RMS_NOSTORE  // (ablation builds: timing only)
-                if (vC) Mo[eC] = m;
+            const uint32_t off = (vC && j < nv) ? (eC + (uint32_t)j * 64u) * 8u : DROP;
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, m[j]), Mr, off, 0, 0);
 #endif
-                eC += 64u;
-                const double d = div_cr(m, Rf, rR);
-                ce = vmax(m, ce - d);
-                De += d;
-            }
+        }
+        eC += (uint32_t)nv * 64u;
+#pragma unroll
+        for (int j = 0; j < B; ++j) {  // (rows past the tile: M = 0 is the identity here)
+            const double mj = j < nv ? m[j] : 0.0;
+            const double d = div_cr(mj, Rf, rR);
+            ce = vmax(mj, ce - d);
+            De += d;
         }
     };
     auto run = [&](auto st, auto &&load) __attribute__((always_inline)) {
@@ -514,15 +531,17 @@ __global__ void __launch_bounds__(256, MM_RMS_MINB) comp_rms_t_kernel(CompArgs a
             for (int j = 0; j < B; ++j) buf[k][j] = load((q + NB) * B + j);
 #pragma unroll
             for (int j = 0; j < B; ++j) Rs[q & 1][j][tlA] = (uint16_t)r[j];
-            if (q > 0) finish_gathers(q - 1);
+            finish_gathers(q - 1);                    // (q = 0: zeros into the idle stage)
             issue_gathers(q);
             __syncthreads();
-            if (q > 0) phase_c(q - 1);
+            phase_c(q - 1);
         };
-        for (int q0 = 0; q0 < NBK; q0 += NB) {
+        // every body issues the same vector memory operations (no conditional loads,
+        // gathers or stores; blocks past the tile are empty), so the compiler's vmcnt
+        // waits count exactly and never wait on the stores
+        for (int q0 = 0; q0 < NBKP; q0 += NB) {
 #pragma unroll
-            for (int k = 0; k < NB; ++k)
-                if (q0 + k < NBK) body(k, q0 + k);
+            for (int k = 0; k < NB; ++k) body(k, q0 + k);
         }
     };
     // (a wave's invalid tiles are its last lanes: lane 0 is valid iff any lane is, so
@@ -531,9 +550,9 @@ __global__ void __launch_bounds__(256, MM_RMS_MINB) comp_rms_t_kernel(CompArgs a
     if (!__any(vA)) run(BoolTag<true>{}, [](int) { return Pair{make_short2(0, 0), make_short2(0, 0)}; });
     else if (steady) run(BoolTag<true>{}, ld_steady);
     else run(BoolTag<false>{}, ld);
-    finish_gathers(NBK - 1);
+    finish_gathers(NBKP - 1);
     __syncthreads();
-    phase_c(NBK - 1);
+    phase_c(NBKP - 1);
     // rows past the tile's frames (the padding to TP) hold M = 0 (identity steps)
     if (vC)
         for (int i = T; i < a.TP; ++i, eC += 64u) Mo[eC] = 0.0;

@@ -27,14 +27,25 @@ struct GateArgs {
     double *out;            // [0] = L, [1] = gain
     const int64_t *trk_blk; // fused batch: block b gates track b's blocks [trk_blk[b], trk_blk[b+1])
                             // into out[2b], out[2b+1]; null: one track, blocks [0, n_blocks)
+    double *zl;             // scratch [2 n_blocks]: z_j, then l_j (gate_blocks_kernel)
 };
 
 constexpr int GATE_THREADS = 1024;
 
-__device__ __forceinline__ double gate_block_z(const GateArgs &a, int64_t j) {
+// z_j and l_j of every block, one thread per block (the segment sum in segment
+// order, as the host restatement): the gate itself then streams them coalesced.
+// (Round 5 computed them inside the one-workgroup gate, a dependent chain of
+// segment loads per block and thread: 220 us for a 2-hour track, 13 us for C2.)
+constexpr int GATE_BLK_THREADS = 256;
+__global__ void __launch_bounds__(GATE_BLK_THREADS) gate_blocks_kernel(GateArgs a) {
+    const int64_t j = (int64_t)blockIdx.x * GATE_BLK_THREADS + threadIdx.x;
+    if (j >= a.n_blocks) return;
+    const int32_t s0 = a.blk_s0[j], s1 = a.blk_s1[j];
     double acc = 0.0;
-    for (int s = a.blk_s0[j]; s < a.blk_s1[j]; ++s) acc += a.seg[s];
-    return a.scale * acc;
+    for (int32_t s = s0; s < s1; ++s) acc += a.seg[s];
+    const double z = a.scale * acc;
+    a.zl[j] = z;
+    a.zl[a.n_blocks + j] = -0.691 + 10.0 * log10(z);
 }
 
 // sum and count over the block, result broadcast to every thread: a fixed-order
@@ -61,8 +72,8 @@ __device__ __forceinline__ void gate_reduce(double &sum, long long &cnt, double 
     __syncthreads();
 }
 
-constexpr int GATE_CACHE = 4;  // block energies a thread keeps between the two gates
-
+// One workgroup per track over its blocks' (z, l) from gate_blocks_kernel: thread t
+// sums blocks t, t + 1024, ... in order, then the fixed-order reduction.
 __global__ void __launch_bounds__(GATE_THREADS) gate_kernel(GateArgs a) {
     __shared__ double rs[GATE_THREADS / 64];
     __shared__ long long rc[GATE_THREADS / 64];
@@ -70,47 +81,12 @@ __global__ void __launch_bounds__(GATE_THREADS) gate_kernel(GateArgs a) {
     const int64_t j0 = a.trk_blk ? a.trk_blk[blockIdx.x] : 0;
     const int64_t j1 = a.trk_blk ? a.trk_blk[blockIdx.x + 1] : a.n_blocks;
     double *out = a.out + 2 * blockIdx.x;
-    double zc[GATE_CACHE], lc[GATE_CACHE];  // the thread's first blocks (a 5-min track: 3 each)
+    const double *zv = a.zl, *lv = a.zl + a.n_blocks;
     double sum = 0.0;
     long long cnt = 0;
-    // the cached blocks first, their segment loads issued together (one latency
-    // instead of a dependent chain per block: the kernel is a single workgroup)
-    int32_t b0[GATE_CACHE], b1[GATE_CACHE];
-#pragma unroll
-    for (int k = 0; k < GATE_CACHE; ++k) {
-        const int64_t j = j0 + t + (int64_t)k * GATE_THREADS;
-        b0[k] = j < j1 ? a.blk_s0[j] : 0;
-        b1[k] = j < j1 ? a.blk_s1[j] : 0;
-    }
-    // (a 0.4 s block spans 4 segments of 0.1 s, 5 at a ragged end: the first four
-    // loads of every block are issued without a wait)
-    double sv[GATE_CACHE][4];
-#pragma unroll
-    for (int k = 0; k < GATE_CACHE; ++k)
-#pragma unroll
-        for (int u = 0; u < 4; ++u) sv[k][u] = b0[k] + u < b1[k] ? a.seg[b0[k] + u] : 0.0;
-#pragma unroll
-    for (int k = 0; k < GATE_CACHE; ++k) {
-        double acc = 0.0;  // segment order, as gate_block_z
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (b0[k] + u < b1[k]) acc += sv[k][u];
-        for (int s_ = b0[k] + 4; s_ < b1[k]; ++s_) acc += a.seg[s_];
-        zc[k] = a.scale * acc;
-    }
-#pragma unroll
-    for (int k = 0; k < GATE_CACHE; ++k) {
-        const int64_t j = j0 + t + (int64_t)k * GATE_THREADS;
-        lc[k] = -0.691 + 10.0 * log10(zc[k]);
-        if (j < j1 && lc[k] >= -70.0) {
-            sum += zc[k];
-            ++cnt;
-        }
-    }
-    int i = GATE_CACHE;
-    for (int64_t j = j0 + t + (int64_t)GATE_CACHE * GATE_THREADS; j < j1; j += GATE_THREADS, ++i) {
-        const double z = gate_block_z(a, j);
-        const double l = -0.691 + 10.0 * log10(z);
+#pragma unroll 8
+    for (int64_t j = j0 + t; j < j1; j += GATE_THREADS) {
+        const double z = zv[j], l = lv[j];
         if (l >= -70.0) {
             sum += z;
             ++cnt;
@@ -121,16 +97,9 @@ __global__ void __launch_bounds__(GATE_THREADS) gate_kernel(GateArgs a) {
     const double gamma_r = -0.691 + 10.0 * log10(mean_abs) - 10.0;
     sum = 0.0;
     cnt = 0;
-    i = 0;
-    for (int64_t j = j0 + t; j < j1; j += GATE_THREADS, ++i) {
-        double z, l;
-        if (i < GATE_CACHE) {
-            z = zc[i];
-            l = lc[i];
-        } else {
-            z = gate_block_z(a, j);
-            l = -0.691 + 10.0 * log10(z);
-        }
+#pragma unroll 8
+    for (int64_t j = j0 + t; j < j1; j += GATE_THREADS) {
+        const double z = zv[j], l = lv[j];
         if (l > gamma_r && l > -70.0) {
             sum += z;
             ++cnt;

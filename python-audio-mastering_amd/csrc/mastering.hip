@@ -793,6 +793,14 @@ static int kweight_energies(mm_ctx *c, const double *carry_in_host, double *seg_
     return chain_check(c, &conv);
 }
 
+// the gate: block energies and levels in parallel, then one workgroup per track
+static int gate_launch(mm_ctx *c, GateArgs ga, unsigned n_tracks) {
+    RET(get_buf(c, "gate_zl", (size_t)(2 * ga.n_blocks), &ga.zl));
+    RET(launch(c, "gate_blocks", gate_blocks_kernel, dim3(blocks_for(ga.n_blocks, GATE_BLK_THREADS)),
+               dim3(GATE_BLK_THREADS), 0, ga));
+    return launch(c, "gate", gate_kernel, dim3(n_tracks), dim3(GATE_THREADS), 0, ga);
+}
+
 // Whole-track loudness and gain on the device (no host round trip).
 static int kweight_device(mm_ctx *c) {
     const mm_job *j = &c->job;
@@ -807,7 +815,7 @@ static int kweight_device(mm_ctx *c) {
     ga.scale = j->block_scale;
     ga.target = j->lufs_target;
     ga.out = c->gate_out;
-    return launch(c, "gate", gate_kernel, dim3(1), dim3(GATE_THREADS), 0, ga);
+    return gate_launch(c, ga, 1);
 }
 
 // pyloudnorm 0.1.1 integrated_loudness gating (mono, G=1), restated.
@@ -1088,7 +1096,7 @@ static int fused_loudness(mm_ctx *c, const mm_job &j0, int n, const FusedPlan &p
     ga.target = j0.lufs_target;
     ga.out = lg;
     ga.trk_blk = p.trk_blk;
-    return launch(c, "gate", gate_kernel, dim3((unsigned)n), dim3(GATE_THREADS), 0, ga);
+    return gate_launch(c, ga, (unsigned)n);
 }
 
 static int fused_finalize(mm_ctx *c, const mm_job *J, int n, const FusedPlan &p, const double *lg, void *const *d_out) {
@@ -1660,7 +1668,7 @@ int mm_gate_finalize_device(mm_ctx *c, const double *d_full, int64_t n_global_se
     ga.scale = block_scale;
     ga.target = target;
     ga.out = gout;
-    RET(launch(c, "gate", gate_kernel, dim3(1), dim3(GATE_THREADS), 0, ga));
+    RET(gate_launch(c, ga, 1));
     RET(finalize(c, 1.0, gout + 1, 1, d_out));
     // L and the gain finalize applied (gate.hip's device expression, not a host recomputation)
     HIPCHK(c, hipMemcpyAsync(loudness_gain_host, gout, 2 * sizeof(double), hipMemcpyDeviceToHost, c->stream));

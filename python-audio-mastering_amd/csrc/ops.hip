@@ -680,7 +680,7 @@ int mm_op_loudness(mm_ctx *c, const mm_job *j, int dtype, const void *in, double
     ga.scale = j->block_scale;
     ga.target = j->lufs_target;
     ga.out = gout;
-    RET(launch(c, "op_gate", gate_kernel, dim3(1), dim3(GATE_THREADS), 0, ga));
+    RET(gate_launch(c, ga, 1));
     HIPCHK(c, hipMemcpyAsync(out, gout, 2 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     resolve_events(c);
