@@ -305,7 +305,9 @@ __global__ void __launch_bounds__(LB_THREADS, 4) eq_kernel(EqArgs a, LbArgs lb, 
     // with the exciter switch as a template argument measured slower: eq 0.152 ->
     // 0.166 ms); pass 2 takes the uniform-row path on full blocks.
     const bool full = (g0 + TPB) * a.T <= a.N_proc;
+#ifndef MM_ABL_EQ_NOP1  // (ablation builds: timing only)
     eq_pass<NS, CH, false, I16>(a, g0, t, c, len, zs, stage);
+#endif
     double z[DIM], s[DIM], rst[DIM];
 #pragma unroll
     for (int s_ = 0; s_ < NS; ++s_) {
@@ -314,13 +316,21 @@ __global__ void __launch_bounds__(LB_THREADS, 4) eq_kernel(EqArgs a, LbArgs lb, 
     }
 #pragma unroll
     for (int d = 0; d < DIM; ++d) rst[d] = 0.0;
+#ifndef MM_ABL_EQ_NOLB  // (ablation builds: timing only)
     lb_carry<DIM, CH>(lb, blk, t, c, valid, valid && (g % line_tiles) == 0, rst, z, s, lds);
+#else
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) s[d] = z[d] + rst[d];
+#endif
     __syncthreads();  // every lane has read the look-back scratch before pass 2 stages into it
 #pragma unroll
     for (int s_ = 0; s_ < NS; ++s_) {
         zs[s_][0] = s[2 * s_];
         zs[s_][1] = s[2 * s_ + 1];
     }
+#ifdef MM_ABL_EQ_NOP2  // (ablation builds: timing only)
+    return;
+#endif
 #ifdef MM_EQ_P2_GENERIC  // (ablation builds)
     if (false) {
 #else

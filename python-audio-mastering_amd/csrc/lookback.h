@@ -181,7 +181,11 @@ __device__ void lb_carry(const LbArgs &a, int blk, int t, int c, bool valid, boo
         for (int d = 0; d < DIM; ++d) sp[d] = 0.0;
     }
     const bool blk_reset = flg[0 * TPB + TPB - 1] != 0;  // same line structure for every channel
+#ifndef MM_ABL_NOLOOK  // (ablation builds: timing only)
     const bool need_carry = !flg[0 * TPB + 0];           // tile 0 of the block is not a line start
+#else
+    const bool need_carry = false;
+#endif
     // 2. publish the aggregate
     if (t == TPB - 1) {
         double *ag = a.agg + ((int64_t)blk * CH + c) * 8;
@@ -204,19 +208,26 @@ __device__ void lb_carry(const LbArgs &a, int blk, int t, int c, bool valid, boo
         bool done = false;
         for (int w = 0; !done; ++w) {
             const int64_t j = (int64_t)blk - 1 - lane - (int64_t)w * LB_WIN;
-            unsigned st = 2u;
-            if (j >= 0) {
-                int spins = 0;
-                st = ld_flag(a.status + j);
-                while (st == 0u) {
-                    __builtin_amdgcn_s_sleep(2);
-                    st = ld_flag(a.status + j);
-                    if (++spins > LB_SPIN_LIMIT) {
+            unsigned st = j >= 0 ? ld_flag(a.status + j) : 2u;
+            // Wait only for the predecessors up to the nearest one with an inclusive
+            // prefix (lanes 0 .. first): the ones past it do not contribute.  (Round 5
+            // waited for all 64 flags of the window, so a block also waited for the
+            // slowest of up to 64 predecessors, the previous chunk's included: eq's
+            // look-back cost 26 us of its 158 on C2)
+            for (int spins = 0;; ++spins) {
+                const unsigned long long inc = __ballot(st == 2u), zero = __ballot(st == 0u);
+                const int first = inc ? __builtin_ctzll(inc) : LB_WIN - 1;
+                const unsigned long long need = first >= 63 ? ~0ull : (2ull << first) - 1ull;
+                if (!(zero & need)) break;
+                if (spins > LB_SPIN_LIMIT) {
+                    if (st == 0u) {
                         st_flag(a.error, 1u);
                         st = 2u;
-                        break;
                     }
+                    break;
                 }
+                __builtin_amdgcn_s_sleep(2);
+                if (st == 0u) st = ld_flag(a.status + j);
             }
             // agent-scope acquire after the polls (cdna_hip_programming.md Guideline 16:
             // ONE relaxed poll, ONE agent acquire, then the loads): this CU's L1 holds
