@@ -1537,6 +1537,11 @@ __global__ void __launch_bounds__(192, MM_APPLY_MINB) comp_apply_kernel(CompArgs
     // a tile without active frames has M = 0 throughout: comp_rms may not have
     // stored its rows (quiet tiles), so it takes 0 instead of loading them
     const bool act = valid && a.cnt[b][g] != 0;
+    // the overlay's fast path: the block's 64 tiles all whole (every block but a
+    // chunk's last and the track's last), so its rows need no per-element bounds
+    const bool full = jn == APPLY_TILES && (g0 + APPLY_TILES) * T <= a.N_proc;
+    const bool stereo = a.ch == 2;
+    short2 *const qrow0 = a.q_out + g0;  // row 0 of the block's first tile
     auto load = [&](int n0, double (&m)[S], short2 (&v)[S], bool with_m) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < S; ++j) {
@@ -1585,7 +1590,15 @@ __global__ void __launch_bounds__(192, MM_APPLY_MINB) comp_apply_kernel(CompArgs
         }
         load(n0 + 2 * S, m, v, !quiet);
         lds_barrier();
-        for (int p = threadIdx.x; p < S * APPLY_TILES; p += 3 * APPLY_TILES) {
+        if (full) {  // every tile of the block whole: wave w takes rows w, w + 3, ... (uniform)
+            const int nv = min(S, T - n0);
+            for (int j = b; j < nv; j += 3) {
+                const short2 lo = lds[0][j][lane], mi = lds[1][j][lane], hi = lds[2][j][lane];
+                const int16_t l = sat16(sat16((int32_t)lo.x + mi.x) + hi.x);
+                const int16_t rr = sat16(sat16((int32_t)lo.y + mi.y) + hi.y);
+                (qrow0 + (int64_t)(n0 + j) * G)[lane] = make_short2(l, stereo ? rr : (int16_t)0);
+            }
+        } else for (int p = threadIdx.x; p < S * APPLY_TILES; p += 3 * APPLY_TILES) {
             const int j = p / APPLY_TILES, tl = p % APPLY_TILES;
             const int64_t gt = g0 + tl;
             const int n = n0 + j;

@@ -64,6 +64,7 @@ struct mm_ctx {
     uint32_t *ctl_claims = nullptr;     // its zeroed claim stamps
     int comp_iters = 0, comp_pending = 0;
     int comp_queue = 0;  // sweeps to queue with the next solve (0: COMP_SWEEPS; then the last solve's need + 1)
+    uint64_t comp_sig = 0;  // settings and geometry of the solve comp_queue was learnt on (comp_signature)
     // loudness on the device
     double *gate_out = nullptr;         // [2]: L, gain
     std::vector<int64_t> geom_cache;    // loudness geometry already on the device
@@ -474,6 +475,29 @@ static int setup_control(mm_ctx *c, unsigned nblk, int64_t nch, int64_t claims) 
 // overlay of the three int16 band planes (tile-major) into q2.  tile_e holds the
 // crossover's per-tile band energies ([3][E, tail][G]).  Queues everything up to
 // the apply; convergence is checked at the chain's sync.
+// FNV-1a over the job fields the envelope solve's sweep count depends on
+static uint64_t comp_signature(const mm_job *j) {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&h](const void *p, size_t n) {
+        const unsigned char *b = static_cast<const unsigned char *>(p);
+        for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+    };
+    mix(&j->frames_proc, sizeof j->frames_proc);
+    mix(&j->rate, sizeof j->rate);
+    mix(&j->tile, sizeof j->tile);
+    mix(&j->tiles_per_chunk, sizeof j->tiles_per_chunk);
+    mix(&j->comp_super, sizeof j->comp_super);
+    for (const mm_band &b : j->band) {
+        mix(&b.thresh_rms, sizeof b.thresh_rms);
+        mix(&b.attack_frames, sizeof b.attack_frames);
+        mix(&b.release_frames, sizeof b.release_frames);
+        mix(&b.look, sizeof b.look);
+        mix(&b.r0, sizeof b.r0);
+        mix(&b.lut_key, sizeof b.lut_key);
+    }
+    return h;
+}
+
 static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], const double *tile_e, short2 **q2_out) {
     const int T = j->tile, ch = j->channels, K = j->tiles_per_chunk;
     const int64_t N = j->frames_proc;
@@ -593,8 +617,16 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
     c->comp_changed = changed;
     c->comp_iters = 0;
     c->comp_pending = 0;
-    // as many as the last solve on this context needed (+ 1 spare): a stream of similar
-    // jobs queues few idle sweeps and rarely resumes from the host
+    // as many as the last solve on this context needed (+ 1 spare) when this job has
+    // the same compressor settings and geometry: a stream of similar jobs queues few
+    // idle sweeps and rarely resumes from the host; a job with other settings or
+    // another length starts from COMP_SWEEPS again (a P_HOT job after P_FULL ones
+    // would otherwise resume from the host)
+    const uint64_t sig = comp_signature(j);
+    if (sig != c->comp_sig) {
+        c->comp_queue = 0;
+        c->comp_sig = sig;
+    }
     int sweeps = c->comp_queue > 0 ? c->comp_queue : COMP_SWEEPS;
     if (const char *e = getenv("MM_COMP_SWEEPS")) sweeps = std::max(1, std::min(16, atoi(e)));  // tests / tuning
     RET(comp_sweeps(c, sweeps));

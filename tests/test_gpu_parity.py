@@ -283,3 +283,40 @@ def test_multiband_at_rate_without_25_frame_tiles(oracle):
     out, info = master_pcm(pcm, rate, P_HOT)
     ref, L = oracle.master(pcm, rate, P_HOT, return_loudness=True)
     _check(out, info, ref, L)
+
+
+def test_sweep_queue_across_settings_on_one_context():
+    """One context, jobs whose settings alternate (P_FULL, P_HOT, P_FULL) and a
+    longer track: the sweep count a context learns from its last solve is reset
+    when the compressor settings or the geometry change (comp_signature), and the
+    output never depends on the context's history (the solve is exact for any
+    number of queued sweeps): every job equals the same job on a fresh context."""
+    import ctypes
+
+    from mastering_amd import Job, native
+    from mastering_amd.engine import _device_input
+    from mastering_amd.synth import pink_noise_pcm16
+    rate = 44100
+
+    def run(ctx, pcm, st):
+        job = Job(pcm.shape[0], rate, 2, st)
+        x, job.job.in_kind = _device_input(pcm)
+        out = np.empty((job.frames_proc, 2), np.int16)
+        res = native.MMResult()
+        ctx.check(ctx.lib.mm_master(ctx.ptr, ctypes.byref(job.job), x.ctypes.data_as(ctypes.c_void_p),
+                                    out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(res)), "mm_master")
+        return out, res
+
+    a = pink_noise_pcm16(40 * rate, rate, 2, 31)
+    b = pink_noise_pcm16(70 * rate, rate, 2, 32)
+    plan = [(a, P_FULL), (a, P_HOT), (a, P_FULL), (b, P_HOT), (a, P_HOT)]
+    shared = native.Context(0)
+    for pcm, st in plan:
+        out, res = run(shared, pcm, st)
+        fresh = native.Context(0)
+        ref, rres = run(fresh, pcm, st)
+        fresh.close()
+        assert np.array_equal(out, ref)
+        assert res.loudness == rres.loudness
+        assert res.comp_iters == rres.comp_iters
+    shared.close()
