@@ -1,8 +1,10 @@
 """Per-block timeline of one eq launch from an MM_EQ_STAMPS build
 (MM_EQ_STAMPS_DUMP=<file>): u64 per block {entry, ticket, pass 1 done, carry
 done, end, HW_ID, -, -} in 100 MHz ticks.  Prints the spread of each phase, the
-look-back wait, the slowest blocks, and and the last blocks to finish.  Usage: python tools/eq_timeline.py <dump>"""
+look-back wait and the last blocks to finish.
+Usage: python tools/eq_timeline.py <dump>"""
 import sys
+
 import numpy as np
 
 d = np.fromfile(sys.argv[1], dtype=np.uint64).reshape(-1, 8)
