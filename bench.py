@@ -37,7 +37,9 @@ whole chunks, extrapolated, on 1 core and on the box's cores; it runs before
 anything touches the GPU (its worker processes are forked).
 
 Run:  python bench.py [--workload C2|C3|C4|C5] [--gpus N] [--steps K] [--warmup W]
-Multi-GPU (driver): python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ... (each rank
+reads RANK / LOCAL_RANK / WORLD_SIZE; --gpus must equal WORLD_SIZE), or `python bench.py
+--gpus N` alone: that process becomes the launcher (launch_ranks) and starts the N ranks itself.
 """
 from __future__ import annotations
 
@@ -125,9 +127,15 @@ def intermediate_bytes(kernel, n, g, active, walked_per_launch):
     return table.get(kernel)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU). Under torch.distributed.run it must equal WORLD_SIZE; without it, "
+                         "N > 1 makes this process a launcher that starts and times N rank processes itself")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher test: every rank prints its rank / local rank / world as JSON and exits "
+                         "before anything touches the GPU")
+    ap.add_argument("--cpu-baseline-from", default=None, help=argparse.SUPPRESS)  # launcher -> rank 0
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="C2")
@@ -143,7 +151,7 @@ def parse():
     ap.add_argument("--tune", action="append", default=[], metavar="NAME=INT",
                     help="tuning experiments only: set engine.NAME (COMP_WARMUP, COMP_SUPER_FRAMES) or "
                          "design.DEFAULT_TILE before the jobs are planned")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
     if args.params is None:
         args.params = WORKLOADS[args.workload].get("params", "full")
     for kv in args.tune:
@@ -350,23 +358,112 @@ def profile_summary(tag):
         return None, path
 
 
-def main():
-    args = parse()
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv) -> int:
+    """`--gpus N` (N > 1) outside torch.distributed.run: this process becomes the
+    launcher.  It runs the CPU baseline (rank 0's leg, before any GPU work), then
+    starts N child processes of this script with RANK = LOCAL_RANK = 0..N-1,
+    WORLD_SIZE = N and a 127.0.0.1 rendezvous, exactly the environment
+    torch.distributed.run would give them; the ranks time themselves (barrier,
+    max over ranks) and rank 0's JSON line is printed here.  The launcher never
+    touches the GPU and never re-execs: the ranks are ordinary child processes,
+    and a failing rank stops the others (by PID) and fails the launch."""
+    import subprocess
+    import tempfile
+    wl, params = WORKLOADS[args.workload], PARAMS[args.params]
+    child_argv = list(argv)
+    tmp = tempfile.mkdtemp(prefix="mm_bench_")
+    if not args.no_cpu_baseline and not args.dry_run:
+        cpu = cpu_baseline(args, wl, params)
+        path = os.path.join(tmp, "cpu_baseline.json")
+        with open(path, "w") as f:
+            json.dump(cpu, f)
+        child_argv += ["--cpu-baseline-from", path]
+    env = dict(os.environ, WORLD_SIZE=str(args.gpus), LOCAL_WORLD_SIZE=str(args.gpus),
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
+    procs, outs = [], []
+    for r in range(args.gpus):
+        out = open(os.path.join(tmp, f"rank{r}.out"), "w+")
+        outs.append(out)
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + child_argv,
+                                      env=dict(env, RANK=str(r), LOCAL_RANK=str(r)), stdout=out))
+    rc = 0
+    pending = set(range(args.gpus))
+    while pending:
+        for r in list(pending):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            pending.discard(r)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                print(f"bench launcher: rank {r} exited with {code}; stopping the other ranks", file=sys.stderr)
+                for q in pending:
+                    procs[q].terminate()
+        time.sleep(0.05)
+    for r, out in enumerate(outs):
+        out.seek(0)
+        text = out.read()
+        out.close()
+        if args.dry_run or r == 0:
+            sys.stdout.write(text)
+        elif text:
+            sys.stderr.write(text)
+    sys.stdout.flush()
+    import shutil
+    shutil.rmtree(tmp, ignore_errors=True)
+    return rc
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus is not None and args.gpus > 1:
+        raise SystemExit(launch_ranks(args, argv))
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = int(env_world or "1")
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch N ranks with "
+                         f"torch.distributed.run --nproc-per-node N, or run bench.py --gpus N alone")
+    if args.dry_run:  # the control plane the timed run uses (gloo rendezvous, max over ranks), no GPU
+        ranks_seen = 1
+        if world > 1:
+            import torch
+            import torch.distributed as dist
+            with stdout_to_stderr():  # gloo prints its connection banner on stdout
+                dist.init_process_group("gloo")
+            t = torch.ones(1)
+            dist.all_reduce(t)
+            ranks_seen = int(t.item())
+            dist.destroy_process_group()
+        print(json.dumps({"rank": rank, "local_rank": local, "world": world, "ranks_in_group": ranks_seen,
+                          "workload": args.workload,
+                          "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}"}), flush=True)
+        return
     wl = WORKLOADS[args.workload]
     params = PARAMS[args.params]
 
     # the CPU baseline first: its worker processes fork before anything initialises the GPU
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and args.cpu_baseline_from:
+        with open(args.cpu_baseline_from) as f:
+            cpu = json.load(f)  # measured by the launcher before it started the ranks
+    elif rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, wl, params)
 
     import torch
     import torch.distributed as dist
     if world > 1:
-        dist.init_process_group("gloo")  # control plane only (barrier, max of timings, RCCL id broadcast)
+        with stdout_to_stderr():  # gloo prints its connection banner on stdout: keep stdout the JSON line
+            dist.init_process_group("gloo")  # control plane only (barrier, max of timings, RCCL id broadcast)
     torch.cuda.set_device(local)
     run = Runner(args, wl, params, rank, world, local, dist if world > 1 else None)
 

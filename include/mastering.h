@@ -118,6 +118,14 @@ typedef struct mm_job {
     int64_t n_segs;          /* distinct boundaries - 1                         */
     const int64_t *seg_bounds; /* host [n_segs+1] sorted distinct block bounds   */
     double block_scale;      /* 1.0 / (0.4 * rate)                              */
+    /* apply_saturation (AME:128-134) tabulated on the int16 grid (ABI 4): host
+       [65536] f32, entry k + 32768 = the reference's expression evaluated by numpy
+       on k / 32768 (AME:121's decoded samples), so the exciter is bit-identical to
+       numpy's float32 tanh wherever the input is a decoded int16 (always on the
+       reference's path); NULL: the device tanhf (within 2 ulp) everywhere.  Inputs
+       off the grid (f32 WAV) always take tanhf. */
+    const float *sat_table;
+    uint64_t sat_key;        /* content key of sat_table (nonzero; cached per context) */
 } mm_job;
 
 typedef struct mm_result {
@@ -154,9 +162,10 @@ int mm_sync(mm_ctx *ctx);
 /* ABI version: 2 = mm_band.lut_key and mm_result.comp_jumped (round 3),
    mm_solve_geometry (round 4); 3 = mm_solve_geom.walk_block, the device loudness
    path in composable steps with a world check and the applied gain returned,
-   device-pointer collectives (round 5).  A caller built against an older header must
+   device-pointer collectives (round 5); 4 = mm_job.sat_table / sat_key and
+   mm_op_saturation_table (round 6).  A caller built against an older header must
    refuse a library whose version differs from its own MM_ABI_VERSION. */
-#define MM_ABI_VERSION 3
+#define MM_ABI_VERSION 4
 int mm_version(void);
 /* The envelope-solve geometry of a job (no context, no GPU).  MM_ERR_ARG if a
    chunk's plane would not fit 32-bit offsets (no track length below 2^31 frames
@@ -255,6 +264,11 @@ int mm_kernel_stats(mm_ctx *ctx, char *names, int names_cap, double *total_ms, i
 int mm_op_pcm_to_float(mm_ctx *ctx, const int16_t *in, int64_t n, float *out);
 /* apply_saturation (AME:128-134); percent != 0 (0 is the identity, no call) */
 int mm_op_saturation(mm_ctx *ctx, int dtype, const void *in, int64_t n, double percent, void *out);
+/* the same with the int16-grid table of mm_job.sat_table (table: [65536] f32, or
+   NULL for the tanhf path): f32 inputs k / 32768 read entry k + 32768, others take
+   tanhf; f64 inputs always compute in f64 */
+int mm_op_saturation_table(mm_ctx *ctx, int dtype, const void *in, int64_t n, double percent, const float *table,
+                           void *out);
 /* apply_stereo_width (AME:136-144) on interleaved stereo [frames][2] */
 int mm_op_stereo_width(mm_ctx *ctx, int dtype, const void *in, int64_t frames, double width, void *out);
 /* float_array_to_audio_segment's samples (AME:123-126): clip, *32768, astype(int16) */

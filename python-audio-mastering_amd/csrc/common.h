@@ -131,7 +131,19 @@ __device__ __forceinline__ void stream2(int len, LD1 &&ld1, LD2 &&ld2, PROC &&pr
 struct SatArgs {
     float keep, mix, drive;
     int on;
+    const float *tab;  // [65536] the reference's apply_saturation on the int16 grid (mm_job.sat_table), or null
 };
+
+// apply_saturation's value for x = k / 32768 from the host table (numpy's float32
+// tanh, bit for bit); false when x is not on the int16 grid (the caller evaluates
+// the expression itself).  x * 32768 is exact; v_cvt_i32_f32 truncates.
+__device__ __forceinline__ bool sat_lookup(float x, const float *tab, float *y) {
+    const float t = x * 32768.0f;
+    const int k = (int)t;
+    if ((float)k != t || k < -32768 || k > 32767) return false;
+    *y = tab[k + 32768];
+    return true;
+}
 
 struct CompArgs {
     int64_t N_proc, G;

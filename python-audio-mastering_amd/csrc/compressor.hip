@@ -13,29 +13,35 @@
 // is held: the step is the identity).
 //
 // The recurrence is solved EXACTLY per (chunk, band) over the chunk's ACTIVE
-// tiles (125 frames; a tile without an active frame holds the state), in
-// super-tiles of TPS consecutive active tiles (1000 frames at 44.1 kHz):
-//  1. comp_rms   per (tile, band): uint16 rms per frame, M = lut[r] gathered ONCE
-//                into a super-tile-major M plane (column blocks of 64, so 64
-//                walkers read 512 contiguous bytes per step), the tile's active
-//                count and largest M;
-//  2. comp_describe per column block: ranks and lists the active tiles (comp_links
-//                until round 3) and
+// tiles (T = 225 frames at 44.1 kHz, design.choose_tile; a tile without an active
+// frame holds the state), in super-tiles of TPS = 4 consecutive active tiles (900
+// frames).  Data flow:
+//  1. comp_rms_t per (column block of 256 tiles, band): exact integer rms per frame
+//                (window sums in doubles, one-sided f32 estimate + one exact check),
+//                M = lut[r] gathered ONCE and stored as f64 into the super-tile-major
+//                M plane (column blocks of 64, so 64 walkers read 512 contiguous
+//                bytes per step), plus per tile its active count, largest M and
+//                (max,+) release summary `ce`, per column block its active-tile count.
+//                Consumers gate every read of M on the tile's count: rows of tiles
+//                with no active frame are never stored (comp_rms's quiet-tile skip).
+//  2. comp_describe per column block: ranks and lists the chunk's active tiles in
+//                compact order and records per active tile the exact effect of its T
+//                release steps on any state of the EIGHT binades above its largest M
+//                (release jumps, JB = 8, both mantissa parities).
 //  3. comp_pass0 walker lanes (one per super-tile, a wave in lockstep) walk from a
-//                guess (the (max,+) release envelope of the preceding active
-//                tiles; exactly 0 at the chunk's first active tile), storing every
-//                tile's entry state and the end; comp_describe (before it) records
-//                per active tile the exact effect of its T release steps on any
-//                state of the four binades above its largest M (release jumps);
+//                guess (the (max,+) release envelope folded over the preceding 32
+//                active tiles; exactly 0 at the chunk's first active tile), storing
+//                every tile's entry state and the end, and compose each full
+//                super-tile's super-jump record.
 //  4. comp_fix   sweeps: a super-tile whose start differs from its predecessor's
-//                end re-walks from it tile by tile — jumped over pure-release
-//                tiles, stepped otherwise — and stops as soon as its state equals
-//                a tile's stored entry state (the stored trajectory from there on
-//                came from the same state).  At the fixed point every start is
-//                its predecessor's end: exact by induction from the chunk start;
-//  5. comp_apply per (tile, band): from the tile's entry state (an inactive tile:
-//                the next active tile's, or the chunk's end), the exact
-//                trajectory, gains, audioop.mul and the overlay through LDS.
+//                end is claimed and re-walked from it — super jumps, release jumps
+//                over pure-release tiles, steps otherwise — and stops as soon as its
+//                state equals a tile's stored entry state (the stored trajectory from
+//                there on came from the same state).  At the fixed point every start
+//                is its predecessor's end: exact by induction from the chunk start.
+//  5. comp_apply per (64 tiles, 3 bands): from the tile's entry state, the exact
+//                trajectory, gains (table exp10), audioop.mul and the overlay
+//                through LDS.
 // Pass 0 needs no warm-up: the true trajectory is in release ~90 % of the time
 // and every stretch between its clamps is crossed by jumps in the sweeps
 // (tools/study/envelope_model.c).

@@ -53,8 +53,13 @@ __device__ __forceinline__ float tanh_sel(float x) {
 }
 
 // apply_saturation (AME:128-134), f32 throughout; no FMA contraction so the
-// rounding sequence matches numpy: keep*x + mix*tanh(x*drive).
+// rounding sequence matches numpy: keep*x + mix*tanh(x*drive).  Inputs on the
+// int16 grid (every decoded PCM16 sample, AME:121) read the host's table of the
+// reference's own numpy evaluation (bit-identical); only off-grid inputs (f32
+// WAV) evaluate tanhf here (within 2 ulp of numpy's float32 tanh).
 __device__ __forceinline__ float saturate(float x, const SatArgs &s) {
+    float y;
+    if (s.tab && sat_lookup(x, s.tab, &y)) return y;
 #ifdef MM_ABLATE_TANH  // timing-only builds (tools/ablate.sh): the exciter without its tanh
     float t = __fmul_rn(x, s.drive);
 #elif defined(MM_TANH_SEL)
@@ -181,7 +186,15 @@ __device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, doub
             }
         }
     };
+    // the exciter runs here, on the staged values (consecutive frames of a tile per
+    // lane group: its table gathers touch few lines), once per sample
     auto store = [&](int buf) {
+        if (a.sat.on) {
+#pragma unroll
+            for (int r = 0; r < ITEMS; ++r)
+#pragma unroll
+                for (int q = 0; q < CH; ++q) regs[r][q] = saturate(regs[r][q], a.sat);
+        }
 #pragma unroll
         for (int r = 0; r < ITEMS; ++r) {
             const int idx = tid + r * LB_THREADS;
@@ -203,8 +216,7 @@ __device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, doub
         for (int j = 0; j < EQ_STAGE; ++j) {
             const int n = step * EQ_STAGE + j;
             if (n >= len) break;
-            float x = row[j * CH + c];
-            if (a.sat.on) x = saturate(x, a.sat);
+            const float x = row[j * CH + c];  // (the exciter's output: applied at staging)
             if (!P2) a.xs[((int64_t)n * a.G + g0 + t) * CH + c] = x;  // pass 2 reads it back coalesced
             double y = (double)x;
 #pragma unroll

@@ -81,6 +81,7 @@ struct mm_ctx {
     std::vector<std::string> stat_order;
     // host tables already resident on the device
     uint64_t lut_key[3] = {0, 0, 0};  // content keys of the band tables on the device (0: none)
+    uint64_t sat_key = 0;             // content key of the exciter table on the device (0: none)
     std::map<std::string, std::vector<double>> mats_cache;
     // pinned block the chain's results are copied into (one sync per chain)
     char *rb = nullptr;
@@ -671,6 +672,16 @@ static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
     ea.sat.mix = j->sat_mix;
     ea.sat.drive = j->sat_drive;
     ea.sat.on = j->sat_on;
+    ea.sat.tab = nullptr;
+    if (j->sat_on && j->sat_table) {  // the exciter's int16-grid table, uploaded when its key changes
+        float *tab;
+        RET(get_buf(c, "sat_tab", 65536, &tab));
+        if (j->sat_key == 0 || c->sat_key != j->sat_key) {
+            HIPCHK(c, hipMemcpyAsync(tab, j->sat_table, 65536 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+            c->sat_key = j->sat_key;
+        }
+        ea.sat.tab = tab;
+    }
     ea.width = j->width;
     ea.width_on = j->width_on && ch == 2;
     ea.q_out = reinterpret_cast<int16_t *>(q1);
@@ -998,6 +1009,7 @@ static bool fusable(const mm_job *J, int n) {
         if (i == 0) continue;
         if (b.channels != a.channels || b.rate != a.rate || b.tile != a.tile || b.tiles_per_chunk != a.tiles_per_chunk ||
             b.sat_keep != a.sat_keep || b.sat_mix != a.sat_mix || b.sat_drive != a.sat_drive || b.sat_on != a.sat_on ||
+            (b.sat_table == nullptr) != (a.sat_table == nullptr) || b.sat_key != a.sat_key ||
             b.width != a.width || b.width_on != a.width_on || b.multiband_on != a.multiband_on ||
             b.lufs_on != a.lufs_on || b.out_kind != a.out_kind || b.in_kind != a.in_kind ||
             b.comp_warmup != a.comp_warmup || b.comp_max_iters != a.comp_max_iters || b.comp_super != a.comp_super)

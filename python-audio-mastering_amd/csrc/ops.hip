@@ -20,11 +20,14 @@ struct PwArgs {
     const void *in;
     void *out;
     double p0, p1, p2;  // op constants (f64; rounded to f32 inside f32 ops)
+    const float *tab;   // PW_SAT on f32: the int16-grid table (mm_op_saturation_table), or null
 };
 
 template <typename T>
-__device__ __forceinline__ T sat_op(T x, double keep, double mix, double drive) {
+__device__ __forceinline__ T sat_op(T x, double keep, double mix, double drive, const float *tab) {
     if constexpr (sizeof(T) == 4) {  // f32: (1-mix)*x + mix*tanh(x*(1+4mix)), constants as f32
+        float y;
+        if (tab && sat_lookup(x, tab, &y)) return y;  // on the int16 grid: numpy's own bits
         const float t = tanhf(__fmul_rn(x, (float)drive));
         return __fadd_rn(__fmul_rn((float)keep, x), __fmul_rn((float)mix, t));
     } else {
@@ -69,7 +72,7 @@ __global__ void __launch_bounds__(256) pointwise_kernel(PwArgs a) {
             const int16_t v = static_cast<const int16_t *>(a.in)[i];
             static_cast<float *>(a.out)[i] = (float)v / 32768.0f;
         } else if constexpr (OP == PW_SAT) {  // apply_saturation (AME:128-134)
-            static_cast<T *>(a.out)[i] = sat_op<T>(static_cast<const T *>(a.in)[i], a.p0, a.p1, a.p2);
+            static_cast<T *>(a.out)[i] = sat_op<T>(static_cast<const T *>(a.in)[i], a.p0, a.p1, a.p2, a.tab);
         } else if constexpr (OP == PW_WIDTH) {  // apply_stereo_width (AME:136-144)
             const T *x = static_cast<const T *>(a.in) + 2 * i;
             T *y = static_cast<T *>(a.out) + 2 * i;
@@ -422,7 +425,8 @@ int mm_op_pcm_to_float(mm_ctx *c, const int16_t *in, int64_t n, float *out) {
                          (size_t)n * 4, pa);
 }
 
-int mm_op_saturation(mm_ctx *c, int dtype, const void *in, int64_t n, double percent, void *out) {
+int mm_op_saturation_table(mm_ctx *c, int dtype, const void *in, int64_t n, double percent, const float *table,
+                           void *out) {
     if (!c || n < 0 || (n > 0 && (!in || !out))) return set_err(c, MM_ERR_ARG, "bad arguments");
     RET(check_dtype(c, dtype));
     HIPCHK(c, hipSetDevice(c->device));
@@ -432,8 +436,18 @@ int mm_op_saturation(mm_ctx *c, int dtype, const void *in, int64_t n, double per
     pa.p0 = 1 - mix;
     pa.p1 = mix;
     pa.p2 = 1 + mix * 4;
+    if (table && dtype == MM_F32) {
+        float *tab;
+        RET(get_buf(c, "op_sat_tab", 65536, &tab));
+        HIPCHK(c, hipMemcpyAsync(tab, table, 65536 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        pa.tab = tab;
+    }
     const size_t bytes = (size_t)n * dtype_size(dtype);
     return PW_DISPATCH(PW_SAT, dtype, in, bytes, out, bytes, pa);
+}
+
+int mm_op_saturation(mm_ctx *c, int dtype, const void *in, int64_t n, double percent, void *out) {
+    return mm_op_saturation_table(c, dtype, in, n, percent, nullptr, out);
 }
 
 int mm_op_stereo_width(mm_ctx *c, int dtype, const void *in, int64_t frames, double width, void *out) {

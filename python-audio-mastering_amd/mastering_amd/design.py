@@ -332,6 +332,29 @@ def loudness_blocks(frames: int, rate: int, block_size: float = 0.4):
     return nblocks, lo, hi, bounds.astype(np.int64), 1.0 / (block_size * rate)
 
 
+@functools.lru_cache(maxsize=16)
+def saturation_table(percent):
+    """apply_saturation (AME:128-134) on the int16 grid: entry k + 32768 is the
+    reference's expression evaluated by numpy on the decoded sample k / 32768
+    (AME:117-121: int16 -> float32 / 2**15), k = -32768..32767.  numpy's float32
+    tanh is a SIMD polynomial that is not correctly rounded, so the device cannot
+    recompute it bit for bit; it gathers these values instead (the per-sample work
+    stays on the GPU; this is host-side design, like max_att_table).  numpy's result
+    is a function of the element's value only (checked in tests/test_ops.py against
+    2-D and strided evaluations), so the table equals the reference's output on
+    every decoded PCM16 sample.  Returns (table float32[65536], content key)."""
+    k = np.arange(-32768, 32768, dtype=np.int32).astype(np.int16)
+    samples = k.astype(np.float32) / (2 ** 15)
+    mix = (percent / 100.0) ** 2
+    clean_signal = samples
+    distorted_signal = np.tanh(samples * (1 + mix * 4))
+    tab = np.ascontiguousarray((1 - mix) * clean_signal + mix * distorted_signal, dtype=np.float32)
+    assert tab.dtype == np.float32 and tab.shape == (65536,)
+    tab.setflags(write=False)
+    key = int.from_bytes(hashlib.blake2b(tab.tobytes(), digest_size=8).digest(), "little") or 1
+    return tab, key
+
+
 def saturation_consts(percent):
     if percent == 0:
         return 0, 1.0, 0.0, 1.0

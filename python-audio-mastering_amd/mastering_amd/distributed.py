@@ -327,8 +327,13 @@ class GpuBackend:
         """Steps 3-5 with torch.distributed ("nccl" = RCCL) summing the library's energy
         vector in place in HBM: the vector is a torch tensor on this context's device."""
         import torch
-        full = torch.zeros(len(plan.seg_bounds) - 1, dtype=torch.float64,
-                           device=torch.device("cuda", self.ctx.device))
+        dev = torch.device("cuda", self.ctx.device)
+        # empty, not zeros: mm_shard_energies_device zeroes the vector on the library's
+        # own (non-blocking) stream; a torch fill would be queued on torch's stream,
+        # unordered with it (ADVICE r05).  Drain torch's stream first so no earlier
+        # torch work on a recycled block can land after the library's writes.
+        full = torch.empty(len(plan.seg_bounds) - 1, dtype=torch.float64, device=dev)
+        torch.cuda.current_stream(dev).synchronize()
         self.shard_energies_device(carry, plan, full.data_ptr())
         coll.all_reduce_sum_device(full)
         return self.gate_finalize_device(full.data_ptr(), plan, target, d_out)
@@ -343,6 +348,15 @@ def master_time_sharded(backend, plan: RankPlan, params: dict, d_in, d_out, coll
     """Run this rank's share of a time-sharded track (steps 1-5 above).
     `d_in` holds the rank's input slice [plan.in_lo, plan.in_hi) (decoded f32);
     `d_out` receives its processed frames [plan.f0, plan.f1)."""
+    # checked before any work or collective: the path depends only on the collective's
+    # kind and the plan, the same on every rank (raises since round 5; see INTEGRATION.md)
+    if isinstance(coll, LibraryCollectives) and (coll.ctx is not getattr(backend, "ctx", None)
+                                                 or coll.world != plan.world):
+        raise ValueError("LibraryCollectives must wrap the backend's own context (its RCCL communicator) "
+                         "over the plan's world")
+    l2g = plan.local_to_global
+    if params.get("lufs") is not None and not (len(l2g) and np.all(np.diff(l2g) == 1)):
+        raise ValueError("a rank's loudness segments must be consecutive global segments")
     job = backend.make_job(plan, params, out_kind)
     backend.stage(job, d_in)
     lufs = params.get("lufs")
@@ -351,14 +365,6 @@ def master_time_sharded(backend, plan: RankPlan, params: dict, d_in, d_out, coll
         z = backend.kweight_range_end()
         zl = coll.all_gather(np.concatenate([z, [float(plan.frames)]]))
         carry = compose_carry(zl[:, :4], zl[:, 4].astype(np.int64), plan.rate, plan.rank)
-        l2g = plan.local_to_global
-        if not (len(l2g) and np.all(np.diff(l2g) == 1)):  # plan_time_shards always makes them consecutive
-            raise ValueError("a rank's loudness segments must be consecutive global segments")
-        # the path depends only on the collective's kind and the plan, the same on every rank
-        if isinstance(coll, LibraryCollectives) and (coll.ctx is not getattr(backend, "ctx", None)
-                                                     or coll.world != plan.world):
-            raise ValueError("LibraryCollectives must wrap the backend's own context (its RCCL communicator) "
-                             "over the plan's world")
         mode = None
         if hasattr(backend, "shard_loudness_device"):
             if isinstance(coll, LibraryCollectives) or (isinstance(coll, LocalCollectives) and plan.world == 1):

@@ -88,6 +88,9 @@ class Job:
         j.channels, j.rate, j.tile, j.tiles_per_chunk = self.channels, self.rate, self.tile, self.tiles_per_chunk
         on, keep, mix, drive = design.saturation_consts(params.get("saturation", 0))
         j.sat_on, j.sat_keep, j.sat_mix, j.sat_drive = on, keep, mix, drive
+        if on:  # the exciter on the int16 grid: numpy's own float32 values (design.saturation_table)
+            self._sat_tab, j.sat_key = design.saturation_table(params.get("saturation", 0))
+            j.sat_table = self._sat_tab.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
         w = params.get("width", 1.0)
         j.width_on = int(w != 1.0 and self.channels == 2)
         j.width = float(w) if w is not None else 1.0

@@ -50,7 +50,8 @@ class MMJob(ctypes.Structure):
                 ("band", MMBand * 3), ("comp_warmup", ctypes.c_int32), ("comp_max_iters", ctypes.c_int32),
                 ("comp_super", ctypes.c_int32), ("in_kind", ctypes.c_int32),
                 ("n_blocks", ctypes.c_int64), ("block_lo", c_int64_p), ("block_hi", c_int64_p),
-                ("n_segs", ctypes.c_int64), ("seg_bounds", c_int64_p), ("block_scale", ctypes.c_double)]
+                ("n_segs", ctypes.c_int64), ("seg_bounds", c_int64_p), ("block_scale", ctypes.c_double),
+                ("sat_table", ctypes.POINTER(ctypes.c_float)), ("sat_key", ctypes.c_uint64)]
 
 
 class MMResult(ctypes.Structure):
@@ -66,7 +67,7 @@ class MMSolveGeom(ctypes.Structure):
                 ("chunk_plane_bytes", ctypes.c_int64), ("plane_bytes", ctypes.c_int64)]
 
 
-ABI_VERSION = 3  # MM_ABI_VERSION of include/mastering.h
+ABI_VERSION = 4  # MM_ABI_VERSION of include/mastering.h
 
 
 class MMWavInfo(ctypes.Structure):
@@ -83,7 +84,7 @@ EXPORTS = ("mm_create", "mm_destroy", "mm_last_error", "mm_sync", "mm_version", 
            "mm_gate_loudness", "mm_finalize",
            "mm_read_mix", "mm_timing", "mm_kernel_stats", "mm_comm_unique_id", "mm_comm_init", "mm_comm_destroy",
            "mm_allreduce_sum_f64", "mm_allgather_f64", "mm_wav_probe", "mm_master_wav",
-           "mm_op_pcm_to_float", "mm_op_saturation", "mm_op_stereo_width", "mm_op_quantize", "mm_op_soft_limiter",
+           "mm_op_pcm_to_float", "mm_op_saturation", "mm_op_saturation_table", "mm_op_stereo_width", "mm_op_quantize", "mm_op_soft_limiter",
            "mm_op_gain", "mm_op_sosfilt", "mm_op_loudness", "mm_op_multiband", "mm_master_batch",
            "mm_op_saturation_legacy", "mm_op_soft_limiter_legacy", "mm_op_sosfilt_mix", "mm_op_compress_bands",
            "mm_solve_geometry")
@@ -145,6 +146,8 @@ def load():
             "mm_allgather_f64_device": ([vp, vp, vp, ctypes.c_int64], ctypes.c_int),
             "mm_op_pcm_to_float": ([vp, vp, ctypes.c_int64, vp], ctypes.c_int),
             "mm_op_saturation": ([vp, ctypes.c_int, vp, ctypes.c_int64, ctypes.c_double, vp], ctypes.c_int),
+            "mm_op_saturation_table": ([vp, ctypes.c_int, vp, ctypes.c_int64, ctypes.c_double,
+                                        ctypes.POINTER(ctypes.c_float), vp], ctypes.c_int),
             "mm_op_stereo_width": ([vp, ctypes.c_int, vp, ctypes.c_int64, ctypes.c_double, vp], ctypes.c_int),
             "mm_op_quantize": ([vp, ctypes.c_int, vp, ctypes.c_int64, vp], ctypes.c_int),
             "mm_op_soft_limiter": ([vp, ctypes.c_int, vp, ctypes.c_int64, ctypes.c_double], ctypes.c_int),

@@ -104,14 +104,20 @@ def float_array_to_audio_segment(float_array, audio_segment_template, device: in
 
 # ------------------------------------------------------------------ pointwise
 def apply_saturation(samples, saturation_percent, device: int = 0):
-    """(1 - mix) x + mix tanh(x (1 + 4 mix)), mix = (s / 100)^2 (AME:128-134)."""
+    """(1 - mix) x + mix tanh(x (1 + 4 mix)), mix = (s / 100)^2 (AME:128-134).
+    float32 samples on the int16 grid (what audio_segment_to_float_array makes)
+    take the values of design.saturation_table (numpy's own float32 tanh); others
+    the device tanhf."""
     if saturation_percent == 0:
         return samples
     x, dt = _float_input(samples, "apply_saturation")
     out = np.empty_like(x)
     ctx = _ctx(device)
-    ctx.check(ctx.lib.mm_op_saturation(ctx.ptr, dt, _ptr(x), x.size, float(saturation_percent), _ptr(out)),
-              "mm_op_saturation")
+    tab = None
+    if dt == native.MM_F32:
+        tab = design.saturation_table(saturation_percent)[0].ctypes.data_as(ctypes.POINTER(ctypes.c_float))
+    ctx.check(ctx.lib.mm_op_saturation_table(ctx.ptr, dt, _ptr(x), x.size, float(saturation_percent), tab,
+                                             _ptr(out)), "mm_op_saturation_table")
     return out
 
 

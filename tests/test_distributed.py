@@ -180,3 +180,36 @@ def test_time_sharded_gloo(tmp_path, oracle, world):
     assert abs(Ls[0][0] - Lref) <= 4e-4
     rms = np.sqrt(np.mean(((out.astype(np.float64) - ref) / 32768) ** 2))
     assert rms <= 1e-5
+
+
+def _small_rank(seconds=3.0):
+    from mastering_amd import distributed as D
+    from mastering_amd.synth import pink_noise_pcm16
+    pcm = pink_noise_pcm16(int(seconds * RATE), RATE, 2, 3)
+    plan = D.plan_time_shards(pcm.shape[0], RATE, 2, 1, 0)
+    return D, pcm, plan, OracleBackend(pcm)
+
+
+def test_time_sharded_refuses_non_consecutive_segments():
+    """a plan whose local segments are not consecutive global ones raises
+    (it used to fall back to the host path silently)."""
+    D, pcm, plan, be = _small_rank()
+    plan.local_to_global = plan.local_to_global.copy()
+    plan.local_to_global[1:] += 1  # a gap after the first segment
+    out = np.empty((plan.frames, 2), np.int16)
+    with pytest.raises(ValueError, match="consecutive"):
+        D.master_time_sharded(be, plan, P_FULL, pcm, out, D.LocalCollectives())
+
+
+@pytest.mark.parametrize("mismatch", ["context", "world"])
+def test_time_sharded_refuses_foreign_library_collectives(mismatch):
+    """LibraryCollectives must wrap the backend's own context over the
+    plan's world; anything else raises instead of taking the host path."""
+    D, pcm, plan, be = _small_rank()
+    be.ctx = object()
+    # no communicator needed: the check comes before any work or collective
+    coll = D.LibraryCollectives(object() if mismatch == "context" else be.ctx,
+                                plan.world + (1 if mismatch == "world" else 0))
+    out = np.empty((plan.frames, 2), np.int16)
+    with pytest.raises(ValueError, match="LibraryCollectives"):
+        D.master_time_sharded(be, plan, P_FULL, pcm, out, coll)

@@ -50,6 +50,28 @@ def test_argument_checks():
         ops.audio_segment_to_float_array(Seg24())
 
 
+@pytest.mark.parametrize("pct", [30, 100, 1, 55.5])
+def test_saturation_table_is_numpys_own(pct, oracle):
+    """design.saturation_table (the exciter's int16-grid table the device gathers) is
+    the reference expression evaluated by numpy: equal, bit for bit, to the oracle's
+    apply_saturation on decoded PCM16 in the reference's [N, 2] layout, in random
+    order and through a strided view (numpy's float32 tanh depends on the value only),
+    and to the primitives fixture the reference's own helper produced."""
+    from mastering_amd import design
+    tab, key = design.saturation_table(pct)
+    assert tab.dtype == np.float32 and tab.shape == (65536,) and key != 0
+    rng = np.random.default_rng(7)
+    pcm = rng.integers(-32768, 32768, size=(200_003, 2)).astype(np.int16)
+    x = oracle.pcm_to_float(pcm)
+    ref = oracle.saturation(x, pct)
+    assert np.array_equal(tab[pcm.astype(np.int32) + 32768], ref)
+    assert np.array_equal(tab[pcm[:, 1].astype(np.int32) + 32768], oracle.saturation(x[:, 1], pct))
+    if pct == 30:
+        prim = np.load(os.path.join(GOLDEN, "primitives.npz"))
+        q = prim["prim_q"].astype(np.int32)
+        assert np.array_equal(tab[q + 32768], prim["prim_sat30"])
+
+
 # ----------------------------------------------------------------- GPU
 class _Seg:
     """pydub-AudioSegment-like (the attributes AME's helpers touch)."""
@@ -84,8 +106,13 @@ def test_saturation(prim):
         y = ops.apply_saturation(got_in, pct)
         ref = prim[key]
         assert y.dtype == ref.dtype == np.float32
+        # on the int16 grid (|k| < 32768 after the x3): the table, numpy's own bits
+        grid = (got_in * 32768 == np.trunc(got_in * 32768)) & (got_in >= -1) & (got_in < 1)
+        assert grid.mean() > 0.3
+        assert np.array_equal(y[grid], ref[grid]), np.mean(y[grid] == ref[grid])
+        record_exact(np.mean(y == ref), "f32")
         ulp = np.spacing(np.abs(ref).astype(np.float32))
-        assert np.all(np.abs(y - ref) <= 2 * ulp), np.max(np.abs(y - ref) / ulp)  # tanh: 2 ulp
+        assert np.all(np.abs(y - ref) <= 2 * ulp), np.max(np.abs(y - ref) / ulp)  # off the grid: tanhf, 2 ulp
 
 
 @pytest.mark.gpu

@@ -126,6 +126,7 @@ def test_rank_of_multi_rank_plan_device_energies_and_gate(coll):
     assert plan.local_to_global[0] > 0 and len(plan.local_to_global) < n_glob
     carry = np.array([1e-3, -2e-3, 5e-4, 1e-4])  # any carry-in state: both paths take the same
     full = torch.full((n_glob,), 7.0, dtype=torch.float64, device="cuda")
+    torch.cuda.current_stream().synchronize()  # the fill is on torch's stream, the library uses its own
     be.shard_energies_device(carry, plan, full.data_ptr())
     got = full.cpu().numpy()
     host = be.hop_energies(carry)
