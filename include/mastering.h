@@ -162,8 +162,8 @@ int mm_sync(mm_ctx *ctx);
 /* ABI version: 2 = mm_band.lut_key and mm_result.comp_jumped (round 3),
    mm_solve_geometry (round 4); 3 = mm_solve_geom.walk_block, the device loudness
    path in composable steps with a world check and the applied gain returned,
-   device-pointer collectives (round 5); 4 = mm_job.sat_table / sat_key and
-   mm_op_saturation_table (round 6).  A caller built against an older header must
+   device-pointer collectives (round 5); 4 = mm_job.sat_table / sat_key,
+   mm_op_saturation_table and mm_np_sum_f32 (round 6).  A caller built against an older header must
    refuse a library whose version differs from its own MM_ABI_VERSION. */
 #define MM_ABI_VERSION 4
 int mm_version(void);
@@ -241,6 +241,11 @@ int mm_shard_loudness_device(mm_ctx *ctx, const double *carry_in_host, int64_t n
 /* Gated loudness from full-track segment energies (host, C restatement of
  * pyloudnorm's gating); returns L via *loudness. */
 int mm_gate_loudness(const mm_job *job, const double *seg_energy, double *loudness);
+/* numpy's float32 np.sum of x[0..n) (n <= 131072), on the host, through the reduction
+ * program the device runs for pyloudnorm's block energies (8192-element buffer
+ * chunks, pairwise leaves of <= 128 with eight accumulators): a CPU check that the
+ * device sums in numpy's order. */
+int mm_np_sum_f32(const float *x, int64_t n, float *out);
 /* Apply gain + soft limiter + quantise (AME:84-89) to the staged mix. */
 int mm_finalize(mm_ctx *ctx, double gain_linear, int use_gain, void *d_out);
 /* Copy the staged pre-gain int16 mix (interleaved) to host (parity probe). */

@@ -132,6 +132,10 @@ struct SatArgs {
     float keep, mix, drive;
     int on;
     const float *tab;  // [65536] the reference's apply_saturation on the int16 grid (mm_job.sat_table), or null
+    // [4096] 2-bit codes per grid entry (16 per word): numpy's value minus the device's
+    // tanhf evaluation, as float bit patterns: 0 equal, 1 +1, 2 -1, 3 other (read tab);
+    // built on the device from tab (sat_corr_kernel), or null (tab alone: a gather per sample)
+    const uint32_t *corr;
 };
 
 // apply_saturation's value for x = k / 32768 from the host table (numpy's float32

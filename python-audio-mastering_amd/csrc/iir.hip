@@ -57,9 +57,8 @@ __device__ __forceinline__ float tanh_sel(float x) {
 // int16 grid (every decoded PCM16 sample, AME:121) read the host's table of the
 // reference's own numpy evaluation (bit-identical); only off-grid inputs (f32
 // WAV) evaluate tanhf here (within 2 ulp of numpy's float32 tanh).
-__device__ __forceinline__ float saturate(float x, const SatArgs &s) {
-    float y;
-    if (s.tab && sat_lookup(x, s.tab, &y)) return y;
+// The device's own evaluation (tanhf: within 2 ulp of numpy's float32 tanh).
+__device__ __forceinline__ float saturate_dev(float x, const SatArgs &s) {
 #ifdef MM_ABLATE_TANH  // timing-only builds (tools/ablate.sh): the exciter without its tanh
     float t = __fmul_rn(x, s.drive);
 #elif defined(MM_TANH_SEL)
@@ -68,6 +67,43 @@ __device__ __forceinline__ float saturate(float x, const SatArgs &s) {
     float t = tanhf(__fmul_rn(x, s.drive));
 #endif
     return __fadd_rn(__fmul_rn(s.keep, x), __fmul_rn(s.mix, t));
+}
+// With the correction codes (the chain's EQ pass 1): the device value, then the
+// 2-bit code of its grid entry from a 16 KB table (a gather touching few cache
+// lines: 512 entries per line) moves it onto numpy's bits; the rare entries that
+// differ by more than one step read the full table.  Without them (pointwise
+// kernels): the full table's entry, a gather per sample.
+__device__ __forceinline__ float saturate(float x, const SatArgs &s) {
+    float y;
+    if (s.corr) {
+        y = saturate_dev(x, s);
+        const float sc = x * 32768.0f;  // exact
+        const int k = (int)sc;
+        if ((float)k == sc && k >= -32768 && k <= 32767) {
+            const unsigned u = (unsigned)(k + 32768);
+            const unsigned code = (s.corr[u >> 4] >> ((u & 15u) * 2u)) & 3u;
+            if (code == 3u) y = s.tab[u];
+            else y = __int_as_float(__float_as_int(y) + (code == 1u ? 1 : (code == 2u ? -1 : 0)));
+        }
+        return y;
+    }
+    if (s.tab && sat_lookup(x, s.tab, &y)) return y;
+    return saturate_dev(x, s);
+}
+
+// Builds SatArgs::corr from SatArgs::tab: thread w packs entries 16w .. 16w + 15.
+__global__ void __launch_bounds__(256) sat_corr_kernel(SatArgs s, uint32_t *corr) {
+    const int w = blockIdx.x * 256 + threadIdx.x;
+    if (w >= 4096) return;
+    uint32_t word = 0;
+    for (int e = 0; e < 16; ++e) {
+        const int u = w * 16 + e;
+        const float x = (float)(u - 32768) * (1.0f / 32768.0f);
+        const int d = __float_as_int(s.tab[u]) - __float_as_int(saturate_dev(x, s));
+        const uint32_t code = d == 0 ? 0u : d == 1 ? 1u : d == -1 ? 2u : 3u;
+        word |= code << (2 * e);
+    }
+    corr[w] = word;
 }
 
 // apply_stereo_width (AME:136-144) on a lane pair, one formula for both lanes:
@@ -89,6 +125,17 @@ __device__ __forceinline__ double widen_pair(double y, double hw) {
 // quantised (AME:63, 204-206) use it, so with the same state they produce
 // scipy's bits.  Otherwise fused (the zero-state passes that only feed the
 // tiles' carry maps).
+// scipy.signal.lfilter's order (_sigtools lfilter.c, one section, a0 == 1): y = Z0 +
+// b0 x; Z0 = (Z1 + x b1) - y a1; Z1 = x b2 - y a2, every product and sum rounded
+// (no contraction: built with -ffp-contract=off).  pyloudnorm's K-weighting
+// filters are lfilter calls (AME:217).
+__device__ __forceinline__ double df2t_lfilter(double x, double &z0, double &z1, const double *c) {
+    const double y = z0 + c[0] * x;
+    z0 = (z1 + x * c[1]) - y * c[3];
+    z1 = x * c[2] - y * c[4];
+    return y;
+}
+
 template <bool SCIPY = false>
 __device__ __forceinline__ double df2t(double x, double &z0, double &z1, const double *c) {
     if constexpr (SCIPY) {
@@ -186,15 +233,7 @@ __device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, doub
             }
         }
     };
-    // the exciter runs here, on the staged values (consecutive frames of a tile per
-    // lane group: its table gathers touch few lines), once per sample
     auto store = [&](int buf) {
-        if (a.sat.on) {
-#pragma unroll
-            for (int r = 0; r < ITEMS; ++r)
-#pragma unroll
-                for (int q = 0; q < CH; ++q) regs[r][q] = saturate(regs[r][q], a.sat);
-        }
 #pragma unroll
         for (int r = 0; r < ITEMS; ++r) {
             const int idx = tid + r * LB_THREADS;
@@ -216,7 +255,8 @@ __device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, doub
         for (int j = 0; j < EQ_STAGE; ++j) {
             const int n = step * EQ_STAGE + j;
             if (n >= len) break;
-            const float x = row[j * CH + c];  // (the exciter's output: applied at staging)
+            float x = row[j * CH + c];
+            if (a.sat.on) x = saturate(x, a.sat);
             if (!P2) a.xs[((int64_t)n * a.G + g0 + t) * CH + c] = x;  // pass 2 reads it back coalesced
             double y = (double)x;
 #pragma unroll
@@ -577,6 +617,12 @@ struct KwArgs {
     int n_trk;
     const int64_t *trk_tile0;  // [n_trk] ascending
     const int64_t *trk_end;    // [n_trk] timeline frame
+    // exact block energies (kw_blocks_kernel): pass 2 writes the f32 square of every
+    // K-weighted frame here instead of segment partials, tile-major like the mix
+    // (frame n of tile g at n * sq_stride + g: coalesced stores) with the row stride
+    // a multiple of 4 (16-byte loads along the tiles)
+    float *sq;
+    int64_t sq_stride;
 };
 
 // pyloudnorm Meter (AME:213-218): mono = f32 mean(L,R) (== (L+R)/65536 exactly),
@@ -585,31 +631,44 @@ struct KwArgs {
 // A lane runs one (sub-)tile of T = Tt / sub frames of a mix tile; the chain uses
 // sub = 1 (5 sub-tiles per tile measured 2x slower: 5x the look-back blocks and
 // 5-line mix loads), the operator path any tile its tables were made for.
-template <bool P2>
+// P2 && SQ: pass 2 in lfilter's own operation order, writing np.square's f32 value
+// of every frame (pyloudnorm squares the f32 filter output, AME:218) for the exact
+// block sums; P2 && !SQ: f64 energies of the (at most two) segments of the tile.
+template <bool P2, bool SQ = false>
 __device__ __forceinline__ void kw_pass(const KwArgs &a, int64_t g, int len, double (&z)[2][2], int64_t seg_end,
                                         int64_t e_end, double &e0, double &e1) {
     const int64_t gt = g / a.sub;  // the mix tile holding sub-tile g, and its first row
     const short2 *mix = reinterpret_cast<const short2 *>(a.mix) + (g - gt * a.sub) * a.T * a.Gt + gt;
     const int64_t Gt = a.Gt;
     int64_t pf = g * a.T;
+    float *sq = SQ ? a.sq + gt + (g - gt * a.sub) * a.T * a.sq_stride : nullptr;
+    const int64_t sqs = SQ ? a.sq_stride : 0;
     stream<8, MM_KW_NB, short2>(
         len, [&](int i) { return mix[(int64_t)min(i, len - 1) * Gt]; },
         [&](short2 q) {
             const float m = a.ch == 2 ? ((float)q.x + (float)q.y) * (1.0f / 65536.0f)
                                       : (float)q.x * (1.0f / 32768.0f);
-            const double y1 = df2t((double)m, z[0][0], z[0][1], a.sos[0]);
-            const float y1f = (float)y1;
-            const double y2 = df2t((double)y1f, z[1][0], z[1][1], a.sos[1]);
-            if (P2) {
-                const float y2f = (float)y2;
-                const double e = pf < e_end ? (double)y2f * (double)y2f : 0.0;
-                if (pf < seg_end) e0 += e;
-                else e1 += e;
+            if constexpr (P2 && SQ) {
+                const float y1f = (float)df2t_lfilter((double)m, z[0][0], z[0][1], a.sos[0]);
+                const float y2f = (float)df2t_lfilter((double)y1f, z[1][0], z[1][1], a.sos[1]);
+                *sq = __fmul_rn(y2f, y2f);
+                sq += sqs;
+            } else {
+                const double y1 = df2t((double)m, z[0][0], z[0][1], a.sos[0]);
+                const float y1f = (float)y1;
+                const double y2 = df2t((double)y1f, z[1][0], z[1][1], a.sos[1]);
+                if (P2) {
+                    const float y2f = (float)y2;
+                    const double e = pf < e_end ? (double)y2f * (double)y2f : 0.0;
+                    if (pf < seg_end) e0 += e;
+                    else e1 += e;
+                }
             }
             ++pf;
         });
 }
 
+template <bool SQ>
 __global__ void __launch_bounds__(LB_THREADS, 2) kweight_kernel(KwArgs a, LbArgs lb) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     __shared__ int ticket_slot;
@@ -638,6 +697,20 @@ __global__ void __launch_bounds__(LB_THREADS, 2) kweight_kernel(KwArgs a, LbArgs
     for (int d = 0; d < 4; ++d) rst[d] = lb.init ? lb.init[d] : 0.0;
     lb_carry<4, 1>(lb, blk, t, 0, valid, valid && g == line0, rst, z, s, smem);
     if (!valid) return;
+    if constexpr (SQ) {
+        zs[0][0] = s[0];
+        zs[0][1] = s[1];
+        zs[1][0] = s[2];
+        zs[1][1] = s[3];
+        kw_pass<true, true>(a, g, len, zs, 0, e_end, e0, e1);
+        if (a.line_end && g == a.G - 1) {
+            a.line_end[0] = zs[0][0];
+            a.line_end[1] = zs[0][1];
+            a.line_end[2] = zs[1][0];
+            a.line_end[3] = zs[1][1];
+        }
+        return;
+    }
     // loudness segment of the tile's first frame (largest s with bounds[s] <= f0)
     const int64_t f0 = g * a.T;
     int64_t lo = 0, hi = a.n_segs;

@@ -70,6 +70,10 @@ struct mm_ctx {
     std::vector<int64_t> geom_cache;    // loudness geometry already on the device
     int32_t *blk_s0 = nullptr, *blk_s1 = nullptr;
     int64_t *seg_bounds_dev = nullptr;
+    // exact block energies (kw_blocks_kernel): per block its first frame and program
+    int64_t *kb_lo = nullptr;
+    int32_t *kb_prog_of = nullptr, *kb_prog = nullptr;
+    std::vector<int64_t> kb_cache;      // block geometry the programs on the device were built for
     // timing
     bool timing = false;
     std::vector<PendingEvent> pending;
@@ -673,14 +677,19 @@ static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
     ea.sat.drive = j->sat_drive;
     ea.sat.on = j->sat_on;
     ea.sat.tab = nullptr;
+    ea.sat.corr = nullptr;
     if (j->sat_on && j->sat_table) {  // the exciter's int16-grid table, uploaded when its key changes
         float *tab;
+        uint32_t *corr;
         RET(get_buf(c, "sat_tab", 65536, &tab));
+        RET(get_buf(c, "sat_corr", 4096, &corr));
+        ea.sat.tab = tab;
         if (j->sat_key == 0 || c->sat_key != j->sat_key) {
             HIPCHK(c, hipMemcpyAsync(tab, j->sat_table, 65536 * sizeof(float), hipMemcpyHostToDevice, c->stream));
+            RET(launch(c, "sat_corr", sat_corr_kernel, dim3(16), dim3(256), 0, ea.sat, corr));
             c->sat_key = j->sat_key;
         }
-        ea.sat.tab = tab;
+        if (!getenv("MM_SAT_GATHER")) ea.sat.corr = corr;  // (A/B: a full-table gather per sample)
     }
     ea.width = j->width;
     ea.width_on = j->width_on && ch == 2;
@@ -776,6 +785,138 @@ static int upload_geometry(mm_ctx *c) {
     return MM_OK;
 }
 
+// ---- numpy's float32 np.sum as a program (gate.hip kw_blocks_kernel) ----------
+// The reduction tree of np.sum over n contiguous float32 values: 8192-element
+// buffer chunks summed in order, each chunk numpy's pairwise recursion (leaves of
+// <= 128 elements).  Serialised as gate.hip's program layout.
+struct PwBuild {
+    std::vector<int32_t> loff, llen;        // leaves in order
+    std::vector<int32_t> na, nb, nh;        // nodes: operands (>= 0 leaf, < 0 node ~k) and height
+    std::vector<int32_t> chunk_leaf;
+};
+static int32_t pw_node(PwBuild &b, int32_t va, int32_t vb, int32_t ha, int32_t hb, int32_t *h) {
+    b.na.push_back(va);
+    b.nb.push_back(vb);
+    *h = std::max(ha, hb) + 1;
+    b.nh.push_back(*h);
+    return ~(int32_t)(b.na.size() - 1);
+}
+static int32_t pw_rec(PwBuild &b, int32_t off, int32_t m, int32_t *h) {
+    if (m <= 128) {  // numpy: m < 8 sequential, else eight accumulators + tail
+        b.loff.push_back(off);
+        b.llen.push_back(m);
+        *h = 0;
+        return (int32_t)b.loff.size() - 1;
+    }
+    int32_t n2 = m / 2;
+    n2 -= n2 % 8;
+    int32_t ha, hb;
+    const int32_t va = pw_rec(b, off, n2, &ha);
+    const int32_t vb = pw_rec(b, off + n2, m - n2, &hb);
+    return pw_node(b, va, vb, ha, hb, h);
+}
+// appends the program of np.sum over n elements to `out`
+static void pw_build(int64_t n, std::vector<int32_t> &out) {
+    PwBuild b;
+    int32_t acc = 0, hacc = 0;
+    const int64_t nch = (n + KB_CHUNK - 1) / KB_CHUNK;
+    for (int64_t c = 0; c < nch; ++c) {
+        b.chunk_leaf.push_back((int32_t)b.loff.size());
+        int32_t h;
+        const int32_t v = pw_rec(b, (int32_t)(c * KB_CHUNK), (int32_t)std::min<int64_t>(KB_CHUNK, n - c * KB_CHUNK), &h);
+        if (c == 0) {  // res = 0 + pairwise(chunk 0): exact (sums of squares are >= +0)
+            acc = v;
+            hacc = h;
+        } else {
+            acc = pw_node(b, acc, v, hacc, h, &hacc);
+        }
+    }
+    b.chunk_leaf.push_back((int32_t)b.loff.size());
+    const int32_t nl = (int32_t)b.loff.size(), nn = (int32_t)b.na.size();
+    // nodes sorted by height (stable): a level reads only lower ones
+    std::vector<int32_t> order(nn), pos(nn);
+    for (int32_t k = 0; k < nn; ++k) order[k] = k;
+    std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return b.nh[x] < b.nh[y]; });
+    for (int32_t k = 0; k < nn; ++k) pos[order[k]] = k;
+    auto vidx = [&](int32_t v) { return v >= 0 ? v : nl + pos[~v]; };
+    const int32_t nlev = nn ? b.nh[order[nn - 1]] : 0;
+    out.push_back(nl);
+    out.push_back(nn);
+    out.push_back(nlev);
+    out.push_back((int32_t)nch);
+    out.push_back(n == 0 ? -1 : vidx(acc));
+    out.insert(out.end(), b.chunk_leaf.begin(), b.chunk_leaf.end());
+    out.insert(out.end(), b.loff.begin(), b.loff.end());
+    out.insert(out.end(), b.llen.begin(), b.llen.end());
+    for (int32_t k = 0; k < nn; ++k) out.push_back(vidx(b.na[order[k]]));
+    for (int32_t k = 0; k < nn; ++k) out.push_back(vidx(b.nb[order[k]]));
+    for (int32_t L = 0, k = 0; L <= nlev; ++L) {  // level L: nodes of height L + 1
+        while (k < nn && b.nh[order[k]] <= L) ++k;
+        out.push_back(k);
+    }
+}
+// The program evaluated on the host with the device's operation order (CPU check
+// against np.sum: mm_np_sum_f32).
+static float pw_eval(const int32_t *P, const float *x) {
+    const int nl = P[0], nn = P[1], nch = P[3], root = P[4];
+    const int32_t *loff = P + 5 + nch + 1, *llen = loff + nl, *na = llen + nl, *nb = na + nn;
+    std::vector<float> val((size_t)nl + nn);
+    for (int li = 0; li < nl; ++li) {
+        const float *e = x + loff[li];
+        const int len = llen[li];
+        float res;
+        if (len < 8) {
+            res = e[0];
+            for (int i = 1; i < len; ++i) res = res + e[i];
+        } else {
+            float r[8];
+            for (int q = 0; q < 8; ++q) r[q] = e[q];
+            int i = 8;
+            for (; i < len - (len & 7); i += 8)
+                for (int q = 0; q < 8; ++q) r[q] = r[q] + e[i + q];
+            res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+            for (; i < len; ++i) res = res + e[i];
+        }
+        val[li] = res;
+    }
+    for (int k = 0; k < nn; ++k) val[nl + k] = val[na[k]] + val[nb[k]];
+    return root < 0 ? 0.0f : val[root];
+}
+
+// Per-block programs on the device: blocks [lo_b, lo_b + n_b) of the line; one
+// program per distinct length (the clamped last blocks of a track differ).
+static int kb_upload(mm_ctx *c, const std::vector<int64_t> &lo, const std::vector<int64_t> &n) {
+    std::vector<int64_t> key(lo);
+    key.insert(key.end(), n.begin(), n.end());
+    const size_t nb = lo.size();
+    RET(get_buf(c, "kb_lo", std::max<size_t>(nb, 1), &c->kb_lo));
+    RET(get_buf(c, "kb_prog_of", std::max<size_t>(nb, 1), &c->kb_prog_of));
+    if (key == c->kb_cache && c->kb_prog) return MM_OK;
+    std::map<int64_t, int32_t> at;
+    std::vector<int32_t> prog, of(nb);
+    for (size_t b = 0; b < nb; ++b) {
+        if (n[b] < 0 || n[b] > 16 * KB_CHUNK) return set_err(c, MM_ERR_ARG, "loudness block of %lld frames", (long long)n[b]);
+        auto it = at.find(n[b]);
+        if (it == at.end()) {
+            const int32_t o = (int32_t)prog.size();
+            pw_build(n[b], prog);
+            if (prog[o] + prog[o + 1] > KB_VMAX) return set_err(c, MM_ERR_ARG, "loudness block program too large");
+            it = at.emplace(n[b], o).first;
+        }
+        of[b] = it->second;
+    }
+    c->kb_prog = nullptr;  // (get_buf may move it: re-fetched below)
+    RET(get_buf(c, "kb_prog", std::max<size_t>(prog.size(), 1), &c->kb_prog));
+    if (nb) {
+        HIPCHK(c, hipMemcpyAsync(c->kb_lo, lo.data(), nb * 8, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->kb_prog_of, of.data(), nb * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->kb_prog, prog.data(), prog.size() * 4, hipMemcpyHostToDevice, c->stream));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // host vectors are transient
+    c->kb_cache = key;
+    return MM_OK;
+}
+
 // K-weighting + per-segment energies of the staged mix (device).  Returns the
 // device segment-energy vector; `line_end` receives the state after the last
 // frame when requested.
@@ -817,9 +958,64 @@ static int kweight_launch(mm_ctx *c, const double *carry_in_host, double *line_e
     ka.part = part;
     ka.part_seg = part_seg;
     ka.line_end = line_end;
-    RET(launch(c, "kweight", kweight_kernel, dim3(nblk), dim3(LB_THREADS), lb_lds_bytes<4, 1>(), ka, lb));
+    RET(launch(c, "kweight", kweight_kernel<false>, dim3(nblk), dim3(LB_THREADS), lb_lds_bytes<4, 1>(), ka, lb));
     RET(launch(c, "seg_reduce", seg_reduce_kernel, dim3(blocks_for(j->n_segs, 4)), dim3(256), 0, ka, seg));  // wave per segment
     *seg_out = seg;
+    return MM_OK;
+}
+
+// The exact loudness of a line (single track or fused timeline, AME:212-218): the
+// K-weighting in lfilter's order writing np.square's f32 values, then pyloudnorm's
+// block energies in numpy's reduction order (kw_blocks_kernel) into zl [2 nb].
+// The block programs must be on the device (kb_upload) before this is queued.
+static int kweight_exact(mm_ctx *c, const mm_job &j0, int64_t frames, int n_trk, const int64_t *trk_tile0,
+                         const int64_t *trk_end, int64_t nb, double **zl_out) {
+    const int64_t G = c->G;
+    const int sub = j0.tile / j0.kweight.tile;  // (design.kweight_sub)
+    const int64_t GS = G * sub;
+    float *sq;
+    double *zl;
+    const int64_t stride = (G + 3) / 4 * 4;  // tile-major rows, 16-byte aligned (kw_blocks' loads)
+    const int Tt = j0.tile;
+    if ((int64_t)Tt * ((KB_CHUNK / Tt + 3) / 4 + 2) > (int64_t)KB_LD * KB_THREADS)
+        return set_err(c, MM_ERR_ARG, "tile of %d frames too long for the loudness block loads", Tt);
+    RET(get_buf(c, "kw_sq", (size_t)(Tt * stride), &sq));
+    RET(get_buf(c, "gate_zl", (size_t)std::max<int64_t>(2 * nb, 2), &zl));
+    LbArgs lb{};
+    RET(upload_tables(c, "kweight", j0.kweight, lb));
+    const unsigned nblk = blocks_for(GS, LB_THREADS);
+    RET(lb_prepare(c, nblk, 1, lb, 2));
+    KwArgs ka{};
+    ka.N_proc = frames;
+    ka.G = GS;
+    ka.T = j0.kweight.tile;
+    ka.Gt = G;
+    ka.sub = sub;
+    ka.ch = j0.channels;
+    for (int s_ = 0; s_ < 2; ++s_)
+        for (int k = 0; k < 5; ++k) ka.sos[s_][k] = j0.kweight.sos[s_][k];
+    ka.mix = reinterpret_cast<const int16_t *>(c->mix);
+    ka.n_trk = n_trk;
+    ka.trk_tile0 = trk_tile0;
+    ka.trk_end = trk_end;
+    ka.sq = sq;
+    ka.sq_stride = stride;
+    RET(launch(c, "kweight", kweight_kernel<true>, dim3(nblk), dim3(LB_THREADS), lb_lds_bytes<4, 1>(), ka, lb));
+    if (nb > 0) {
+        KbArgs kb{};
+        kb.sq = sq;
+        kb.sq_stride = stride;
+        kb.T = Tt;
+        kb.n_blocks = nb;
+        kb.blk_lo = c->kb_lo;
+        kb.blk_prog = c->kb_prog_of;
+        kb.prog = c->kb_prog;
+        kb.scale = (float)j0.block_scale;  // Python float * np.float32: the constant rounded to f32 (NEP 50)
+        kb.zl = zl;
+        const unsigned grid = (unsigned)((nb + 7) / 8 * 8);  // a multiple of 8 (the XCD-aware block mapping)
+        RET(launch(c, "kw_blocks", kw_blocks_kernel, dim3(grid), dim3(KB_THREADS), 0, kb));
+    }
+    *zl_out = zl;
     return MM_OK;
 }
 
@@ -836,29 +1032,58 @@ static int kweight_energies(mm_ctx *c, const double *carry_in_host, double *seg_
     return chain_check(c, &conv);
 }
 
-// the gate: block energies and levels in parallel, then one workgroup per track
+// the gate: block energies and levels from the segment energies in parallel (unless
+// ga.zl already holds them: the exact path), then one workgroup per track
 static int gate_launch(mm_ctx *c, GateArgs ga, unsigned n_tracks) {
-    RET(get_buf(c, "gate_zl", (size_t)(2 * ga.n_blocks), &ga.zl));
-    RET(launch(c, "gate_blocks", gate_blocks_kernel, dim3(blocks_for(ga.n_blocks, GATE_BLK_THREADS)),
-               dim3(GATE_BLK_THREADS), 0, ga));
+    if (!ga.zl) {
+        RET(get_buf(c, "gate_zl", (size_t)(2 * ga.n_blocks), &ga.zl));
+        RET(launch(c, "gate_blocks", gate_blocks_kernel, dim3(blocks_for(ga.n_blocks, GATE_BLK_THREADS)),
+                   dim3(GATE_BLK_THREADS), 0, ga));
+    }
     return launch(c, "gate", gate_kernel, dim3(n_tracks), dim3(GATE_THREADS), 0, ga);
 }
 
-// Whole-track loudness and gain on the device (no host round trip).
+// Whole-track loudness and gain on the device (no host round trip), exactly
+// pyloudnorm's block energies.
 static int kweight_device(mm_ctx *c) {
     const mm_job *j = &c->job;
-    double *seg;
-    RET(kweight_launch(c, nullptr, nullptr, &seg));
+    if (getenv("MM_LOUDNESS_SEGMENTS")) {  // (A/B builds: round 5's f64 segment energies)
+        double *seg;
+        RET(kweight_launch(c, nullptr, nullptr, &seg));
+        GateArgs ga{};
+        ga.n_blocks = j->n_blocks;
+        ga.blk_s0 = c->blk_s0;
+        ga.blk_s1 = c->blk_s1;
+        ga.seg = seg;
+        ga.scale = j->block_scale;
+        ga.target = j->lufs_target;
+        ga.out = c->gate_out;
+        return gate_launch(c, ga, 1);
+    }
+    {
+        std::vector<int64_t> lo(j->block_lo, j->block_lo + j->n_blocks), n((size_t)j->n_blocks);
+        for (int64_t b = 0; b < j->n_blocks; ++b) n[b] = j->block_hi[b] - j->block_lo[b];
+        RET(kb_upload(c, lo, n));
+    }
+    double *zl;
+    RET(kweight_exact(c, *j, j->frames_proc, 0, nullptr, nullptr, j->n_blocks, &zl));
     // c->gate_out: in the control block's readback area (setup_control)
     GateArgs ga{};
     ga.n_blocks = j->n_blocks;
-    ga.blk_s0 = c->blk_s0;
-    ga.blk_s1 = c->blk_s1;
-    ga.seg = seg;
-    ga.scale = j->block_scale;
     ga.target = j->lufs_target;
     ga.out = c->gate_out;
+    ga.zl = zl;
     return gate_launch(c, ga, 1);
+}
+
+// numpy's float32 np.sum over x[0..n) evaluated on the host through the same
+// program the device runs for pyloudnorm's block energies (CPU check of pw_build).
+extern "C" int mm_np_sum_f32(const float *x, int64_t n, float *out) {
+    if (!out || n < 0 || (n > 0 && !x) || n > 16 * KB_CHUNK) return MM_ERR_ARG;
+    std::vector<int32_t> prog;
+    pw_build(n, prog);
+    *out = pw_eval(prog.data(), x);
+    return MM_OK;
 }
 
 // pyloudnorm 0.1.1 integrated_loudness gating (mono, G=1), restated.
@@ -1076,6 +1301,15 @@ static int fused_geometry(mm_ctx *c, const mm_job *J, int n, FusedPlan *p) {
         tend[i] = o + j.frames_proc;
     }
     tblk[n] = (int64_t)s0.size();
+    {  // the exact path's blocks: every track's own blocks at its timeline offset
+        std::vector<int64_t> lo, len;
+        for (int i = 0; i < n; ++i)
+            for (int64_t b = 0; b < J[i].n_blocks; ++b) {
+                lo.push_back(p->off[i] + J[i].block_lo[b]);
+                len.push_back(J[i].block_hi[b] - J[i].block_lo[b]);
+            }
+        RET(kb_upload(c, lo, len));
+    }
     if (bounds.back() < p->P) bounds.push_back(p->P);  // the last track's padding
     p->n_segs = (int64_t)bounds.size() - 1;
     p->n_blocks = (int64_t)s0.size();
@@ -1100,6 +1334,17 @@ static int fused_geometry(mm_ctx *c, const mm_job *J, int n, FusedPlan *p) {
 // K-weighting (a line per track), segment energies and per-track gating into
 // lg[2i] = L, lg[2i+1] = gain.
 static int fused_loudness(mm_ctx *c, const mm_job &j0, int n, const FusedPlan &p, double *lg) {
+    if (!getenv("MM_LOUDNESS_SEGMENTS")) {  // exact block energies (the programs: fused_geometry)
+        double *zl;
+        RET(kweight_exact(c, j0, p.P, n, p.trk_tile0, p.trk_end, p.n_blocks, &zl));
+        GateArgs ga{};
+        ga.n_blocks = p.n_blocks;
+        ga.target = j0.lufs_target;
+        ga.out = lg;
+        ga.trk_blk = p.trk_blk;
+        ga.zl = zl;
+        return gate_launch(c, ga, (unsigned)n);
+    }
     const int64_t G = c->G;
     const int sub = j0.tile / j0.kweight.tile;  // (design.kweight_sub)
     const int64_t GS = G * sub;
@@ -1129,7 +1374,7 @@ static int fused_loudness(mm_ctx *c, const mm_job &j0, int n, const FusedPlan &p
     ka.n_trk = n;
     ka.trk_tile0 = p.trk_tile0;
     ka.trk_end = p.trk_end;
-    RET(launch(c, "kweight", kweight_kernel, dim3(nblk), dim3(LB_THREADS), lb_lds_bytes<4, 1>(), ka, lb));
+    RET(launch(c, "kweight", kweight_kernel<false>, dim3(nblk), dim3(LB_THREADS), lb_lds_bytes<4, 1>(), ka, lb));
     RET(launch(c, "seg_reduce", seg_reduce_kernel, dim3(blocks_for(p.n_segs, 4)), dim3(256), 0, ka, seg));
     GateArgs ga{};
     ga.n_blocks = p.n_blocks;
