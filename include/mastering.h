@@ -152,6 +152,8 @@ typedef struct mm_solve_geom {
     int64_t chunk_plane_bytes; /* one chunk's part of one band's M plane: walked
                                 through 32-bit buffer offsets, < 2^31           */
     int64_t plane_bytes;     /* the three bands' M planes of the whole track     */
+    int32_t col_block;       /* columns per comp_rms workgroup / pass-0 wave (64) (ABI 4) */
+    int32_t rms_group_tiles; /* tiles per comp_rms workgroup: tps * col_block (ABI 4) */
 } mm_solve_geom;
 
 /* ---- context ------------------------------------------------------------ */
@@ -163,13 +165,15 @@ int mm_sync(mm_ctx *ctx);
    mm_solve_geometry (round 4); 3 = mm_solve_geom.walk_block, the device loudness
    path in composable steps with a world check and the applied gain returned,
    device-pointer collectives (round 5); 4 = mm_job.sat_table / sat_key,
-   mm_op_saturation_table and mm_np_sum_f32 (round 6).  A caller built against an older header must
+   mm_op_saturation_table, mm_np_sum_f32, mm_solve_geom.col_block / rms_group_tiles
+   (round 6).  A caller built against an older header must
    refuse a library whose version differs from its own MM_ABI_VERSION. */
 #define MM_ABI_VERSION 4
 int mm_version(void);
 /* The envelope-solve geometry of a job (no context, no GPU).  MM_ERR_ARG if a
    chunk's plane would not fit 32-bit offsets (no track length below 2^31 frames
-   at rates up to 192 kHz does). */
+   at rates up to 192 kHz does) or if comp_super is not 4 tiles (the rms kernel's
+   workgroup shape). */
 int mm_solve_geometry(const mm_job *job, mm_solve_geom *out);
 /* sha256 prefix (16 hex digits) of the sources this library was built from
    (mastering_amd/srcsha.py: the csrc sources and this header) */

@@ -60,20 +60,6 @@ __device__ __forceinline__ uint32_t frame_energy(short2 v) {
     return (uint32_t)((int32_t)v.x * v.x) + (uint32_t)((int32_t)v.y * v.y);
 }
 
-// largest r with n*r*r <= S (== isqrt(S div n) == trunc(sqrt(S/n)) computed in
-// doubles, tests/test_oracle.py).  S and n*r*r are integers below 2^53, so the
-// f64 products and compares are exact.  The f32 estimate (v_sqrt_f32 of S * 1/n, a
-// few ulp relative: < 0.01 absolute at r <= 32768) is within 1 of r, which the two
-// exact checks correct.
-__device__ __forceinline__ uint32_t rms_exact(double S, double n, float inv_n) {
-    int32_t r = (int32_t)__builtin_amdgcn_sqrtf((float)S * inv_n);
-    double rd = (double)r;
-    r -= (n * rd * rd > S) ? 1 : 0;
-    rd = (double)(r + 1);
-    r += (n * rd * rd <= S) ? 1 : 0;
-    return n > 0.0 ? (uint32_t)r : 0u;
-}
-
 // correctly rounded m / d given rd = RN(1/d) (Markstein; tests/test_oracle.py)
 __device__ __forceinline__ double div_cr(double m, double d, double rd) {
     const double q = m * rd;
@@ -85,6 +71,7 @@ __device__ __forceinline__ double div_cr(double m, double d, double rd) {
 #define MM_RMS_NB 3
 #endif
 constexpr int RMS_B = 8;  // frames per load block of comp_rms
+constexpr int RMS_TPS = 4;  // tiles per super-tile comp_rms_t is written for (its four waves)
 
 // Super-tile-major M plane of a band: frame n of tile g — the k-th tile of
 // super-tile s — is row k*TP + n of column s (TP = T rounded up to whole walk load
@@ -157,197 +144,6 @@ __device__ __forceinline__ double vmax(double x, double y) {
     asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
     return r;
 }
-
-// Lanes of a wave take 64 CONSECUTIVE tiles (wave w of column block cb: tiles
-// 64 TPS cb + 64 w + lane of the chunk), so every band load is one 256-byte run and,
-// in the steady state (no lane in its chunk's first `look` frames, every tile
-// whole), the frame row of a load and of its drop frame is the same for all lanes:
-// a scalar row base plus the lane's tile.  M stores go to the super-tile-major
-// plane as before (four 128-byte runs per wave store: 16 columns at each of the
-// TPS = 4 tile positions).  The per-frame exact rms needs one correction
-// (rms_exact1); energies are single v_dot2 instructions.
-__global__ void __launch_bounds__(256, MM_RMS_MINB) comp_rms_kernel(CompArgs a) {
-    const int b = blockIdx.y;
-    const int64_t wv = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const int64_t cbk = wv / a.TPS;                 // global column block
-    const int wq = (int)(wv - cbk * a.TPS);
-    const int64_t cc = (cbk * 64) / a.SPC;          // its chunk (SPC: whole column blocks)
-    const int64_t jt = (cbk * 64 - cc * a.SPC) * a.TPS + (int64_t)wq * 64 + lane;  // tile in the chunk
-    const int64_t g = cc * a.K + jt;
-    if (jt >= a.K || g >= a.G) return;  // past the chunk's tiles or the track
-    const int64_t sc = cc * a.SPC + jt / a.TPS;     // its column
-    const int kc = (int)(jt % a.TPS);
-    const short2 *x = a.band[b];
-    const int look = a.look[b];
-    const int T = a.T;
-    const uint32_t G = (uint32_t)a.G, g32 = (uint32_t)g;
-    const int64_t f0 = g * T;
-    const int64_t chunk0 = cc * a.K * T;
-    const int len = (int)min((int64_t)T, a.N_proc - f0);
-    const int64_t lo0 = max(chunk0, f0 - look);
-    double S = 0.0;
-    {
-        const int kf = look / T;
-        for (int t = 1; t <= kf; ++t)
-            if ((g - t) * T >= chunk0) S += a.E[b][g - t];
-        if (look % T != 0 && (g - kf - 1) * T >= chunk0) S += a.tail[b][g - kf - 1];
-    }
-    const int64_t d_first = max(f0 - look, chunk0);
-    const int skip = (int)(d_first - (f0 - look));
-    const uint32_t gd = (uint32_t)(d_first / T);
-    const int nd = (int)(d_first - (int64_t)gd * T);
-    const int ch = a.ch;
-    double n = (double)((f0 - lo0) * ch);
-    float inv = n > 0.0 ? rcp_biased(n) : 0.f;
-    const uint32_t r0 = a.r0[b];
-    const double *lut = a.lut[b];
-    const double Rf = a.release_frames[b], rR = a.rcp_release[b];
-    constexpr uint32_t GS32 = 64;
-    double *Mo = chunk_plane(a, b, cc);
-    uint32_t e = col_elem(a, sc) + (uint32_t)(kc * a.TP) * GS32;
-    int i_proc = 0, active = 0;
-    uint32_t rmx = 0;
-    struct Pair {
-        short2 in, drop;
-    };
-    // steady waves: uniform rows; the drop frame of frame i is row (nd + i) mod T of
-    // tile gd (+1 past the wrap), gd - g the same for every lane
-    const bool steady = __all(skip == 0 && len == T && look > 0);
-    // (uniform when steady: taken from the first lane so the row bases live in SGPRs)
-    const int64_t dgo = (int64_t)__builtin_amdgcn_readfirstlane((int)((int64_t)gd - g));
-    const int nd_u = __builtin_amdgcn_readfirstlane(nd);
-    auto ld_steady = [&](int i) {
-        i = min(i, T - 1);
-        Pair p;
-        p.in = (x + (int64_t)i * G)[g32];
-        int k = nd_u + i;
-        const int wrap = k >= T ? 1 : 0;
-        k -= wrap * T;
-        p.drop = (x + (int64_t)k * G + dgo + wrap)[g32];
-        return p;
-    };
-    auto ld = [&](int i) {
-        i = min(i, len - 1);
-        Pair p;
-        p.in = x[(uint32_t)i * G + g32];
-        int k = nd + max(i - skip, 0);
-        const int wrap = k >= T ? 1 : 0;
-        k -= wrap * T;
-        p.drop = x[(uint32_t)k * G + gd + (uint32_t)wrap];
-        return p;
-    };
-    auto rms_step = [&](Pair p, auto st) __attribute__((always_inline)) {
-        uint32_t r;
-        if constexpr (decltype(st)::value) {
-            r = rms_exact1(S, n, inv);
-            S += (double)frame_energy2(p.in) - (double)frame_energy2(p.drop);
-        } else {
-            r = n > 0.0 ? rms_exact1(S, n, inv) : 0u;
-            const bool drops = i_proc >= skip;
-            S += (double)frame_energy2(p.in) - (drops ? (double)frame_energy2(p.drop) : 0.0);
-            if (!drops) {  // window still growing (first `look` frames of a chunk only)
-                n += ch;
-                inv = rcp_biased(n);
-            }
-            ++i_proc;
-        }
-        active += r >= r0 ? 1 : 0;
-        rmx = max(rmx, r);
-        return r;
-    };
-    constexpr int B = RMS_B, NB = MM_RMS_NB;
-    Pair buf[NB][B];
-    double mq[B];
-    int pn = 0;
-    double ce = 0.0, De = 0.0;
-    auto flush = [&](bool whole) __attribute__((always_inline)) {
-#pragma unroll
-        for (int j = 0; j < B; ++j)
-            if (whole || j < pn) {
-#ifndef MM_RMS_NOSTORE  // (ablation builds: timing only)
-                Mo[e + (uint32_t)j * GS32] = mq[j];
-#endif
-                const double d = div_cr(mq[j], Rf, rR);
-                ce = vmax(mq[j], ce - d);
-                De += d;
-            }
-        e += (uint32_t)pn * GS32;
-    };
-    auto run = [&](auto st, auto &&load, int L) __attribute__((always_inline)) {
-#pragma unroll
-        for (int k = 0; k < NB; ++k) {
-#pragma unroll
-            for (int j = 0; j < B; ++j) buf[k][j] = load(k * B + j);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        auto block = [&](int k, int q, int nv) __attribute__((always_inline)) {
-            uint32_t r[B];
-#pragma unroll
-            for (int j = 0; j < B; ++j) r[j] = j < nv ? rms_step(buf[k][j], st) : 0u;
-            double m[B];
-#pragma unroll
-            for (int j = 0; j < B; ++j)
-#ifdef MM_RMS_NOGATHER  // (ablation builds: timing only)
-                m[j] = (double)r[j];
-#else
-                m[j] = lut[r[j]];
-#endif
-            __builtin_amdgcn_sched_barrier(0);
-            if (q > 0) flush(true);
-#pragma unroll
-            for (int j = 0; j < B; ++j) buf[k][j] = load((q + NB) * B + j);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int j = 0; j < B; ++j) mq[j] = m[j];
-            pn = nv;
-        };
-        const int nfull = L / B, ntail = L - nfull * B;
-        int q = 0;
-        for (; q + NB <= nfull; q += NB) {
-#pragma unroll
-            for (int k = 0; k < NB; ++k) block(k, q + k, B);
-        }
-#pragma unroll
-        for (int k = 0; k < NB; ++k)
-            if (q + k < nfull) block(k, q + k, B);
-        if (ntail) {
-#pragma unroll
-            for (int k = 0; k < NB; ++k)
-                if (k == nfull % NB) block(k, nfull, ntail);
-        }
-        flush(false);
-    };
-    // A tile whose largest possible window sum (S at its start plus every frame that
-    // enters during it; drops only lower it) stays below n r0^2 has no active frame
-    // (r >= r0 iff n r0^2 <= S; integers below 2^53 in f64): its M rows are all 0,
-    // and no kernel reads them (comp_describe and the solve walk active tiles only,
-    // comp_apply takes M = 0 for a tile without active frames), so it loads,
-    // gathers and stores nothing.  (n is fixed once the window is full.)
-    const bool quiet = skip == 0 && (double)n * ((double)r0 * (double)r0) > S + a.E[b][g];
-    if (!quiet) {
-        if (steady) run(BoolTag<true>{}, ld_steady, T);
-        else if (len > 0) run(BoolTag<false>{}, ld, len);
-        for (int i = max(len, 0); i < a.TP; ++i, e += GS32) Mo[e] = 0.0;
-    }
-    a.cnt[b][g] = active;
-    a.mmax[b][g] = lut[rmx];
-    {  // active tiles of the column block (the wave's tiles share it)
-        const int na = (int)__popcll(__ballot(active != 0));
-        if (__lane_id() == __builtin_amdgcn_readfirstlane(__lane_id()) && na)
-            atomicAdd(a.cbtot[b] + (sc >> 6), na);
-    }
-    reinterpret_cast<double2 *>(a.ced[b])[g] = make_double2(ce, De);
-    const int c = (int)cc;
-    if (__ballot(1) == ~0ull) {
-        int v = active;
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-        if (__lane_id() == 0 && v) atomicAdd(a.total[b] + c, v);
-    } else if (active) {
-        atomicAdd(a.total[b] + c, active);
-    }
-}
-
 
 // ---- comp_rms with the table gathers and M stores transposed through LDS -------
 // (TPS == 4: a workgroup = one column block = 256 consecutive tiles of a chunk.)

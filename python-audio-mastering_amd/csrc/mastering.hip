@@ -441,6 +441,9 @@ static int solve_geometry(const mm_job *j, mm_solve_geom *g) {
     const int64_t G = (j->frames_proc + T - 1) / T;
     *g = mm_solve_geom{};
     g->tps = std::max(1, std::min((j->comp_super + T / 2) / T, DESC_MAX_TPS));  // (comp_describe: 64 TPS threads)
+    if (g->tps != RMS_TPS) return MM_ERR_ARG;  // comp_rms_t's workgroup: RMS_TPS positions x 64 columns
+    g->col_block = 64;
+    g->rms_group_tiles = RMS_TPS * 64;
     g->chunks = (G + K - 1) / K;
     g->cols_per_chunk = (((int64_t)K + g->tps - 1) / g->tps + 63) / 64 * 64;
     g->walk_block = WB;
@@ -610,10 +613,8 @@ static int stage_compress(mm_ctx *c, const mm_job *j, short2 *const bands[3], co
         ca.se0[b] = ca.sjump ? se0s + (size_t)b * NS : nullptr;
         ca.cbtot[b] = reinterpret_cast<int32_t *>(claims + (size_t)3 * NS) + (size_t)b * (NS / 64);
     }
-    if (ca.TPS == 4 && !getenv("MM_RMS_V2"))  // column block = one workgroup: gathers / stores through LDS
-        RET(launch(c, "comp_rms", comp_rms_t_kernel, dim3((unsigned)(NS / 64), 3), dim3(256), 0, ca));
-    else
-        RET(launch(c, "comp_rms", comp_rms_kernel, dim3(blocks_for(NS / 64 * ca.TPS, 4), 3), dim3(256), 0, ca));
+    // column block = one workgroup (RMS_TPS x 64 tiles): gathers / stores through LDS
+    RET(launch(c, "comp_rms", comp_rms_t_kernel, dim3((unsigned)(NS / 64), 3), dim3(256), 0, ca));
     RET(launch(c, "comp_describe", comp_describe_kernel, dim3((unsigned)(NS / 64), 3), dim3(64 * ca.TPS), 0, ca));
     RET(launch(c, "comp_pass0", comp_pass0_kernel, dim3(blocks_for(NS, PASS0_BLOCK), 3), dim3(PASS0_BLOCK), 0, ca));
     c->comp_on = true;

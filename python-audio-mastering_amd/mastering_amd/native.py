@@ -64,7 +64,8 @@ class MMResult(ctypes.Structure):
 class MMSolveGeom(ctypes.Structure):
     _fields_ = [("tps", ctypes.c_int32), ("tile_rows", ctypes.c_int32), ("rows", ctypes.c_int32),
                 ("walk_block", ctypes.c_int32), ("cols_per_chunk", ctypes.c_int64), ("chunks", ctypes.c_int64),
-                ("chunk_plane_bytes", ctypes.c_int64), ("plane_bytes", ctypes.c_int64)]
+                ("chunk_plane_bytes", ctypes.c_int64), ("plane_bytes", ctypes.c_int64),
+                ("col_block", ctypes.c_int32), ("rms_group_tiles", ctypes.c_int32)]
 
 
 ABI_VERSION = 4  # MM_ABI_VERSION of include/mastering.h

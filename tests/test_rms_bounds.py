@@ -5,32 +5,42 @@ or the track, which load as lane 0 does) and every M-plane store (phase C: T row
 plus the padding to whole walk blocks) stays inside its buffer.  Round 5 found a
 negative drop index for such invalid lanes this way (a GPU fault on a 40 s track);
 the model restates the kernel's index arithmetic at the geometries the product
-uses (design.choose_tile, 4-tile super-tiles, 64-column blocks)."""
+uses.  The geometry (tile, tiles per super-tile, columns per chunk and per
+workgroup, rows per tile and per column) comes from the library's own planning
+function mm_solve_geometry for a planned Job, not restated here, so the model
+follows the kernel when its geometry moves."""
+import ctypes
+
 import pytest
 
-from mastering_amd import design
+from mastering_amd import engine, native
+
+
+def _geometry(frames, rate):
+    job = engine.Job(frames, rate, 2, {"multiband": True})
+    g = native.MMSolveGeom()
+    assert native.load().mm_solve_geometry(ctypes.byref(job.job), ctypes.byref(g)) == 0
+    return job, g
 
 
 def _check(frames, rate, look, prefetch=24):
-    chunk = 30 * rate
-    T = design.choose_tile(chunk)
-    K = chunk // T
-    N = frames
+    job, geo = _geometry(frames, rate)
+    T, K, N = job.tile, job.tiles_per_chunk, job.frames_proc
     G = (N + T - 1) // T
-    TPS = 4
-    SPC = ((K + TPS - 1) // TPS + 63) // 64 * 64
-    NS = ((G + K - 1) // K) * SPC
-    WB = design.WALK_BLOCK
-    TP = (T + WB - 1) // WB * WB
-    RP = TPS * TP + 2 * WB
-    chunk_elems = RP * SPC
+    TPS, CB = geo.tps, geo.col_block
+    assert geo.rms_group_tiles == TPS * CB == 256  # comp_rms_t: 256 threads, lane = tile in phase A
+    SPC = geo.cols_per_chunk
+    NS = geo.chunks * SPC
+    TP, RP = geo.tile_rows, geo.rows
+    chunk_elems = geo.chunk_plane_bytes // 8
+    assert chunk_elems == RP * SPC
     band_len = T * G
     bad = []
-    for cbk in range(NS // 64):
-        cc = (cbk * 64) // SPC
-        jt0 = (cbk * 64 - cc * SPC) * 4
+    for cbk in range(NS // CB):
+        cc = (cbk * CB) // SPC
+        jt0 = (cbk * CB - cc * SPC) * TPS
         chunk0 = cc * K * T
-        for w in range(4):
+        for w in range(TPS):
             lanes = [(jt0 + w * 64 + l, cc * K + jt0 + w * 64 + l) for l in range(64)]
             valid = [jt < K and g < G for jt, g in lanes]
             if not any(valid):
@@ -60,14 +70,14 @@ def _check(frames, rate, look, prefetch=24):
                         wrap = int(k >= T)
                         idx = (ii * G + g32, (k - wrap * T) * G + gd + wrap)
                     bad += [("load", cbk, w, i, x) for x in idx if not 0 <= x < band_len]
-        for w in range(4):
-            for lane in range(64):
-                jt = jt0 + lane * 4 + w
+        for w in range(TPS):
+            for lane in range(CB):
+                jt = jt0 + lane * TPS + w
                 if jt >= K or cc * K + jt >= G:
                     continue
-                sl = (cc * SPC + jt // 4) % SPC
-                e = (sl >> 6) * RP * 64 + (sl & 63) + w * TP * 64
-                if not (e >= 0 and e + (TP - 1) * 64 < chunk_elems):
+                sl = (cc * SPC + jt // TPS) % SPC
+                e = (sl // CB) * RP * CB + (sl % CB) + w * TP * CB
+                if not (e >= 0 and e + (TP - 1) * CB < chunk_elems):
                     bad.append(("store", cbk, w, lane, e))
     return bad
 
