@@ -14,6 +14,8 @@
 // segment energies (f64) on the time-sharded and per-stage paths (gate_blocks).
 // The reductions over blocks are tree-ordered (the result differs from numpy's
 // pairwise mean in the last bits only: ~1e-16 of the gain).
+#include <type_traits>
+
 #include "common.h"
 
 namespace mm {
@@ -49,113 +51,206 @@ constexpr int GATE_THREADS = 1024;
 // values 0..nleaves-1 are the leaves, nleaves + k node k = val[a] + val[b]; nodes are
 // sorted by height so each level only reads earlier ones.
 struct KbArgs {
-    const float *sq;          // tile-major f32 squares of the K-weighted line (kweight_kernel<true>)
-    int64_t sq_stride;        // its row stride (tiles, a multiple of 4)
-    int T;                    // frames per tile
+    const float *sq;          // f32 squares of the K-weighted line, tile g at g * TP (kweight_kernel<true>)
+    int T, TP;                // frames per tile, padded tile stride (a multiple of 4)
     int64_t n_blocks;
     const int64_t *blk_lo;    // first frame of each block
+    const int32_t *blk_n;     // its length
     const int32_t *blk_prog;  // its program (int offset into prog)
     const int32_t *prog;
     float scale;              // f32(1 / (0.4 rate))
     double *zl;               // [2 n_blocks]: z_j, then l_j (read by gate_kernel)
+    int stage_floats, nvals, pints;  // dynamic LDS layout (kb_lds_bytes: nvals = both value buffers), pints % 4 == 0
 };
 constexpr int KB_CHUNK = 8192;   // numpy's reduction buffer (elements)
-constexpr int KB_VMAX = 2048;    // leaves + nodes of one block (76 800 frames at 192 kHz: ~1200)
+constexpr int KB_VMAX = 1536;    // leaves + nodes of one block (76 800 frames at 192 kHz: 1199)
+constexpr int KB_PMAX = 2560;    // ints of one program (192 kHz: 2430); programs start 16-byte aligned
 constexpr int KB_THREADS = 256;
-constexpr int KB_LD = 13;        // 16-byte loads per thread per chunk: rows T <= 512 x (8192/T + 8)/4 tile quads
-__host__ __device__ constexpr int kb_pad(int i) { return i + 4 * (i >> 7); }  // 128-element runs 4 banks apart
+constexpr int KB_LD = 9;         // 16-byte loads per thread per chunk: padded tile quads of the tiles a
+                                 // chunk spans, (8191 / T + 2) * ceil(T / 4) <= 2304 (host-checked)
 
-// One workgroup per block; consecutive blocks on one XCD (their windows overlap
-// 3/4: the re-reads hit that XCD's L2).  Per 8192-element chunk: the chunk's
-// frames are staged in LDS (16-byte loads of 4 tiles at a row, the next chunk's
-// loads in flight while this one is summed), four lanes per leaf run numpy's eight
-// accumulators (two each), then the program's levels combine the leaves in numpy's
-// order.
+// Dynamic LDS of kw_blocks_kernel: the staged chunk (frame order), the leaf/node
+// values (two buffers), the program.
+// chunk index -> LDS word: 8 words of padding per 128 frames (a wave's 16 leaves
+// start 128 frames apart: with the padding their 8-word groups fill 64 banks twice)
+__host__ __device__ constexpr int kb_pad(int i) { return i + ((i >> 7) << 3); }
+__host__ __device__ constexpr int kb_lds_bytes(int stage_floats, int nvals, int pints) {
+    return stage_floats * 4 + ((nvals + 3) / 4 * 4) * 4 + pints * 4;
+}
+
+// Persistent workgroups: workgroup w of XCD x (x = w % 8) takes the blocks
+// x per + w/8, + grid/8, ... of its XCD's contiguous range (neighbouring blocks'
+// windows overlap 3/4: the re-reads hit that XCD's L2).  The blocks' chunks
+// (8192 frames, numpy's buffers) form one stream over all the workgroup's blocks
+// with KB_RING chunks' 16-byte loads in flight (a ring of register buffers).  Per chunk the frames are copied to
+// LDS in frame order (8 words of padding per 128 frames: kb_pad); eight lanes per
+// leaf run numpy's eight accumulators; per block the
+// program's levels combine the leaves in numpy's order.  A block's program (one
+// per block length) stays in LDS while the next block has the same.
+#ifndef MM_KB_RING
+#define MM_KB_RING 1
+#endif
+constexpr int KB_RING = MM_KB_RING;  // chunks in flight per workgroup (1-3)
 __global__ void __launch_bounds__(KB_THREADS) kw_blocks_kernel(KbArgs a) {
-    __shared__ __attribute__((aligned(16))) float el[kb_pad(KB_CHUNK)];
-    __shared__ float val[KB_VMAX];
-    const unsigned per = gridDim.x / 8;  // (the grid is a multiple of 8)
-    const int64_t j = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
-    if (j >= a.n_blocks) return;  // (workgroup-uniform)
+    extern __shared__ __attribute__((aligned(16))) float kb_smem[];
+    __shared__ int kb_prog_cur;
     const int tid = threadIdx.x;
-    const int32_t *P = a.prog + a.blk_prog[j];
-    const int nl = P[0], nn = P[1], nlev = P[2], nch = P[3], root = P[4];
-    const int32_t *chunk_leaf = P + 5, *loff = chunk_leaf + nch + 1, *llen = loff + nl, *na = llen + nl,
-                  *nb = na + nn, *lvl = nb + nn;
-    const int64_t lo = a.blk_lo[j];
-    const int T = a.T;
+    float *el = kb_smem;
+    float *val = kb_smem + a.stage_floats;
+    int32_t *P = reinterpret_cast<int32_t *>(val + (a.nvals + 3) / 4 * 4);
+    const int64_t nbk = a.n_blocks;
+    const int64_t per = (nbk + 7) / 8;
+    const int xcd = (int)(blockIdx.x % 8), nslot = (int)(gridDim.x / 8);
+    const int64_t jb = xcd * per + blockIdx.x / 8, je = min((int64_t)(xcd + 1) * per, nbk);
+    if (jb >= je) return;  // (workgroup-uniform)
+    const int T = a.T, Q4 = a.TP / 4;  // frames per tile, 16-byte quads per padded tile
     const float4 *sq4 = reinterpret_cast<const float4 *>(a.sq);
-    const int64_t rs4 = a.sq_stride / 4;
-    float4 buf[KB_LD];
-    int64_t gq0 = 0;   // the staged chunk's first tile quad
-    int nq = 0;        // its tile quads per row
-    auto issue = [&](int c) __attribute__((always_inline)) {  // chunk c's loads into buf
-        const int64_t F0 = lo + (int64_t)c * KB_CHUNK;
-        const int m = loff[chunk_leaf[c + 1] - 1] + llen[chunk_leaf[c + 1] - 1] - c * KB_CHUNK;
-        gq0 = (F0 / T) >> 2;
-        nq = (int)(((F0 + m - 1) / T >> 2) - gq0 + 1);
+    if (tid == 0) kb_prog_cur = -1;
+    // a thread's (tile, quad) of its first load in a chunk and the step between its loads
+    const int t_0 = tid / Q4, k_0 = tid - (tid / Q4) * Q4;
+    const int dt = KB_THREADS / Q4, dk = KB_THREADS - (KB_THREADS / Q4) * Q4;
+    float4 buf[KB_RING][KB_LD];
+    int g_i0[KB_RING], g_m[KB_RING], g_nld[KB_RING];  // per buffer: chunk index of its first tile's
+                                                      // frame 0 (<= 0), length, quads loaded
+    // the stream's next chunk: (block lj, chunk lc)
+    int64_t lj = jb;
+    int lc = 0;
+    int64_t lF0 = a.blk_lo[lj];
+    int ln = a.blk_n[lj];
+    while (ln <= 0 && lj < je) {
+        lj += nslot;
+        if (lj < je) lF0 = a.blk_lo[lj], ln = a.blk_n[lj];
+    }
+    auto issue = [&](auto B) __attribute__((always_inline)) {  // the stream's next chunk into buffer B
+        constexpr int b = decltype(B)::value;
+        if (lj >= je) return;
+        const int m = min(KB_CHUNK, ln - lc * KB_CHUNK);
+        const int64_t F0 = lF0 + (int64_t)lc * KB_CHUNK;
+        const int64_t tA = F0 / T;
+        const int nld = (int)((F0 + m - 1) / T - tA + 1) * Q4;
+        g_i0[b] = (int)(tA * T - F0);
+        g_m[b] = m;
+        g_nld[b] = nld;
+        const float4 *base = sq4 + tA * Q4;
+        int t = t_0, k = k_0;
 #pragma unroll
         for (int r = 0; r < KB_LD; ++r) {
-            const int k = tid + r * KB_THREADS;
-            const int n = k / nq, q = k - n * nq;
-            buf[r] = n < T ? sq4[(int64_t)n * rs4 + gq0 + q] : make_float4(0.f, 0.f, 0.f, 0.f);
+            buf[b][r] = base[min(t * Q4 + k, nld - 1)];  // (past the chunk: reloaded, not stored)
+            t += dt;
+            k += dk;
+            if (k >= Q4) {
+                k -= Q4;
+                ++t;
+            }
+        }
+        if (++lc * KB_CHUNK >= ln) {  // advance (blocks without frames have no chunks)
+            lc = 0;
+            for (lj += nslot; lj < je; lj += nslot) {
+                lF0 = a.blk_lo[lj];
+                ln = a.blk_n[lj];
+                if (ln > 0) break;
+            }
         }
     };
-    if (nch > 0) issue(0);
-    for (int c = 0; c < nch; ++c) {
-        const int l0 = chunk_leaf[c], l1 = chunk_leaf[c + 1];
-        const int64_t F0 = lo + (int64_t)c * KB_CHUNK;
-        const int m = loff[l1 - 1] + llen[l1 - 1] - c * KB_CHUNK;  // the chunk's length
+    auto copy = [&](auto B) __attribute__((always_inline)) {  // buffer B -> LDS in frame order
+        constexpr int b = decltype(B)::value;
+        const int m = g_m[b], nld = g_nld[b], i_t0 = g_i0[b];
+        int t = t_0, k = k_0;
 #pragma unroll
         for (int r = 0; r < KB_LD; ++r) {
-            const int k = tid + r * KB_THREADS;
-            const int n = k / nq, q = k - n * nq;
-            const int64_t i0 = ((gq0 + q) * 4) * T + n - F0;  // chunk index of tile 4(gq0+q), row n
-            const float e4[4] = {buf[r].x, buf[r].y, buf[r].z, buf[r].w};
+            const float4 v = buf[b][r];
+            const int i = i_t0 + t * T + 4 * k;  // chunk index of the quad's first frame
+            const bool ld = t * Q4 + k < nld;
+            if (ld && i >= 0 && i + 3 < m && 4 * k + 3 < T) {  // (the common case: all four)
+                el[kb_pad(i)] = v.x, el[kb_pad(i + 1)] = v.y, el[kb_pad(i + 2)] = v.z, el[kb_pad(i + 3)] = v.w;
+            } else if (ld) {
+                const float e4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int64_t i = i0 + (int64_t)e * T;
-                if (n < T && i >= 0 && i < m) el[kb_pad((int)i)] = e4[e];
+                for (int e = 0; e < 4; ++e)
+                    if (i + e >= 0 && i + e < m && 4 * k + e < T) el[kb_pad(i + e)] = e4[e];
+            }
+            t += dt;
+            k += dk;
+            if (k >= Q4) {
+                k -= Q4;
+                ++t;
             }
         }
-        __syncthreads();
-        if (c + 1 < nch) issue(c + 1);  // in flight while this chunk is summed
-        const int q = tid & 3;          // accumulators 2q, 2q + 1 of the leaf
-        for (int li = l0 + (tid >> 2); li < l1; li += KB_THREADS / 4) {
-            const int off = loff[li] - c * KB_CHUNK, len = llen[li];
-            float res;
-            if (len < 8) {  // (a chunk shorter than 8: numpy's sequential sum; lane 0 of the four)
-                res = el[kb_pad(off)];
-                for (int i = 1; i < len; ++i) res = __fadd_rn(res, el[kb_pad(off + i)]);
-            } else {
-                float2 r = *reinterpret_cast<const float2 *>(el + kb_pad(off) + 2 * q);
-                const int full = len - (len & 7);
-                int i = 8;
-                for (; i < full; i += 8) {
-                    const float2 v = *reinterpret_cast<const float2 *>(el + kb_pad(off + i) + 2 * q);
-                    r.x = __fadd_rn(r.x, v.x);
-                    r.y = __fadd_rn(r.y, v.y);
+    };
+    issue(std::integral_constant<int, 0>{});
+    if constexpr (KB_RING > 1) issue(std::integral_constant<int, 1 % KB_RING>{});
+    if constexpr (KB_RING > 2) issue(std::integral_constant<int, 2 % KB_RING>{});
+    int ring = 0;  // the buffer holding the next chunk to sum
+    int vb = 0;    // val double buffer: the levels of block j read val[vb] while block j+1 fills the other
+    for (int64_t j = jb; j < je; j += nslot, vb ^= 1) {
+        const int pj = a.blk_prog[j];
+        __syncthreads();  // (everyone is done with P, el and this val buffer's previous block)
+        if (pj != kb_prog_cur) {  // a new program into LDS (the device buffer is padded by pints ints)
+            const int4 *src = reinterpret_cast<const int4 *>(a.prog + pj);
+            int4 *dst = reinterpret_cast<int4 *>(P);
+            for (int i = tid; i < a.pints / 4; i += KB_THREADS) dst[i] = src[i];
+            __syncthreads();
+            if (tid == 0) kb_prog_cur = pj;
+        }
+        const int nl = P[0], nn = P[1], nlev = P[2], nch = P[3], root = P[4];
+        const int32_t *chunk_leaf = P + 5, *loff = chunk_leaf + nch + 1, *llen = loff + nl, *na = llen + nl,
+                      *nb = na + nn, *lvl = nb + nn;
+        float *V = val + vb * ((a.nvals + 1) / 2);  // (nvals counts both buffers)
+        for (int c = 0; c < nch; ++c) {
+            const int l0 = chunk_leaf[c], l1 = chunk_leaf[c + 1];
+            // this chunk from its ring buffer into LDS, then that buffer takes the stream's
+            // chunk three ahead (static buffer indices: no register array indexing)
+            if (KB_RING == 1 || ring == 0) copy(std::integral_constant<int, 0>{});
+            else if (KB_RING == 2 || ring == 1) copy(std::integral_constant<int, 1 % KB_RING>{});
+            else copy(std::integral_constant<int, 2 % KB_RING>{});
+            __syncthreads();
+            if (KB_RING == 1 || ring == 0) issue(std::integral_constant<int, 0>{});
+            else if (KB_RING == 2 || ring == 1) issue(std::integral_constant<int, 1 % KB_RING>{});
+            else issue(std::integral_constant<int, 2 % KB_RING>{});
+            ring = ring == KB_RING - 1 ? 0 : ring + 1;
+            const int q = tid & 7;  // accumulator q of the leaf (eight lanes per leaf)
+            for (int li = l0 + (tid >> 3); li < l1; li += KB_THREADS / 8) {
+                const int off = loff[li] - c * KB_CHUNK, len = llen[li];
+                float res;
+                if (len < 8) {  // (a chunk shorter than 8: numpy's sequential sum)
+                    res = el[kb_pad(off)];
+                    for (int i = 1; i < len; ++i) res = __fadd_rn(res, el[kb_pad(off + i)]);
+                } else {
+                    float r;
+                    const int full = len - (len & 7);
+                    if (full == 128 && (off & 127) == 0) {  // the common leaf: one padded run, reads issued at once
+                        const float *e = el + kb_pad(off) + q;
+                        float v[16];
+#pragma unroll
+                        for (int g = 0; g < 16; ++g) v[g] = e[8 * g];
+                        r = v[0];
+#pragma unroll
+                        for (int g = 1; g < 16; ++g) r = __fadd_rn(r, v[g]);
+                    } else {  // (8-aligned groups never straddle a 128-frame run)
+                        r = el[kb_pad(off) + q];
+                        for (int i = 8; i < full; i += 8) r = __fadd_rn(r, el[kb_pad(off + i) + q]);
+                    }
+                    // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)): f32 addition commutes, so every
+                    // lane of the eight ends with the same bits
+                    r = __fadd_rn(r, __shfl_xor(r, 1));
+                    r = __fadd_rn(r, __shfl_xor(r, 2));
+                    res = __fadd_rn(r, __shfl_xor(r, 4));
+                    for (int i = full; i < len; ++i) res = __fadd_rn(res, el[kb_pad(off + i)]);
                 }
-                // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)); f32 addition commutes, so every lane
-                // of the four ends with the same bits
-                float p = __fadd_rn(r.x, r.y);
-                p = __fadd_rn(p, __shfl_xor(p, 1));
-                res = __fadd_rn(p, __shfl_xor(p, 2));
-                for (; i < len; ++i) res = __fadd_rn(res, el[kb_pad(off + i)]);
+                if (q == 0) V[li] = res;
             }
-            if (q == 0) val[li] = res;
+            __syncthreads();  // (the next chunk overwrites el; the levels read V)
         }
-        __syncthreads();  // (the next chunk overwrites el)
-    }
-    for (int L = 0; L < nlev; ++L) {
-        for (int k = lvl[L] + tid; k < lvl[L + 1]; k += KB_THREADS) val[nl + k] = __fadd_rn(val[na[k]], val[nb[k]]);
-        __syncthreads();
-    }
-    if (tid == 0) {
-        const float s = root < 0 ? 0.0f : val[root];
-        const double z = (double)__fmul_rn(a.scale, s);
-        a.zl[j] = z;
-        a.zl[a.n_blocks + j] = -0.691 + 10.0 * log10(z);
+        for (int L = 0; L < nlev; ++L) {
+            for (int k = lvl[L] + tid; k < lvl[L + 1]; k += KB_THREADS) V[nl + k] = __fadd_rn(V[na[k]], V[nb[k]]);
+            __syncthreads();
+        }
+        if (tid == 0) {
+            const float sm = root < 0 ? 0.0f : V[root];
+            const double z = (double)__fmul_rn(a.scale, sm);
+            a.zl[j] = z;
+            a.zl[nbk + j] = -0.691 + 10.0 * log10(z);
+        }
     }
 }
 

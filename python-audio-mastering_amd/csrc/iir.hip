@@ -68,42 +68,59 @@ __device__ __forceinline__ float saturate_dev(float x, const SatArgs &s) {
 #endif
     return __fadd_rn(__fmul_rn(s.keep, x), __fmul_rn(s.mix, t));
 }
-// With the correction codes (the chain's EQ pass 1): the device value, then the
-// 2-bit code of its grid entry from a 16 KB table (a gather touching few cache
-// lines: 512 entries per line) moves it onto numpy's bits; the rare entries that
-// differ by more than one step read the full table.  Without them (pointwise
-// kernels): the full table's entry, a gather per sample.
+// With the correction codes: the device value, then the 2-bit code of its grid
+// entry moves it onto numpy's bits; the rare entries more than one step apart read
+// the full table.  The codes are one table for |k| (both the device's and numpy's
+// values are odd in x; sat_corr_kernel marks an entry 3 where the two signs
+// disagree): 2049 words, 8 KB (the EQ kernel gathers them at staging).  Without them
+// (pointwise operators): the full table's entry, a gather per sample.
+// The codes are only used when no entry is 3 (sat_corr_kernel's exception flag,
+// checked on the host once per table): then the exciter issues no global load in
+// the EQ's per-frame loop (a conditional one there made the compiler drain the
+// staging prefetch at every frame).
+__device__ __forceinline__ float saturate_corr(float x, const SatArgs &s, const uint32_t *corr) {
+    float y = saturate_dev(x, s);
+    const float sc = x * 32768.0f;  // exact
+    const int k = (int)sc;
+    if ((float)k == sc && k >= -32768 && k <= 32767) {
+        const unsigned u = (unsigned)abs(k);
+        const unsigned code = k == -32768 ? s.code_m : (corr[u >> 4] >> ((u & 15u) * 2u)) & 3u;
+        y = __int_as_float(__float_as_int(y) + (int)(code & 1u) - (int)(code >> 1));
+    }
+    return y;
+}
 __device__ __forceinline__ float saturate(float x, const SatArgs &s) {
     float y;
-    if (s.corr) {
-        y = saturate_dev(x, s);
-        const float sc = x * 32768.0f;  // exact
-        const int k = (int)sc;
-        if ((float)k == sc && k >= -32768 && k <= 32767) {
-            const unsigned u = (unsigned)(k + 32768);
-            const unsigned code = (s.corr[u >> 4] >> ((u & 15u) * 2u)) & 3u;
-            if (code == 3u) y = s.tab[u];
-            else y = __int_as_float(__float_as_int(y) + (code == 1u ? 1 : (code == 2u ? -1 : 0)));
-        }
-        return y;
-    }
+    if (s.corr) return saturate_corr(x, s, s.corr);
     if (s.tab && sat_lookup(x, s.tab, &y)) return y;
     return saturate_dev(x, s);
 }
 
-// Builds SatArgs::corr from SatArgs::tab: thread w packs entries 16w .. 16w + 15.
-__global__ void __launch_bounds__(256) sat_corr_kernel(SatArgs s, uint32_t *corr) {
+constexpr int SAT_CORR_WORDS = 2048;  // |k| = 0 .. 32767, 16 codes per word (8 KB)
+// Builds SatArgs::corr from SatArgs::tab: thread w packs |k| = 16w .. 16w + 15;
+// exceptions[0] counts entries that need the table, exceptions[1] = k = -32768's code.
+__global__ void __launch_bounds__(256) sat_corr_kernel(SatArgs s, uint32_t *corr, unsigned *exceptions) {
     const int w = blockIdx.x * 256 + threadIdx.x;
-    if (w >= 4096) return;
+    if (w >= SAT_CORR_WORDS) return;
+    auto code_of = [&](int k) {
+        const float x = (float)k * (1.0f / 32768.0f);
+        const int d = __float_as_int(s.tab[k + 32768]) - __float_as_int(saturate_dev(x, s));
+        return d == 0 ? 0u : d == 1 ? 1u : d == -1 ? 2u : 3u;
+    };
     uint32_t word = 0;
     for (int e = 0; e < 16; ++e) {
         const int u = w * 16 + e;
-        const float x = (float)(u - 32768) * (1.0f / 32768.0f);
-        const int d = __float_as_int(s.tab[u]) - __float_as_int(saturate_dev(x, s));
-        const uint32_t code = d == 0 ? 0u : d == 1 ? 1u : d == -1 ? 2u : 3u;
+        const uint32_t cp = code_of(u), cn = code_of(-u);
+        const uint32_t code = cp == cn ? cp : 3u;
         word |= code << (2 * e);
+        if (code == 3u) atomicAdd(exceptions, 1u);
     }
     corr[w] = word;
+    if (w == 0) {
+        const uint32_t cm = code_of(-32768);
+        exceptions[1] = cm;
+        if (cm == 3u) atomicAdd(exceptions, 1u);
+    }
 }
 
 // apply_stereo_width (AME:136-144) on a lane pair, one formula for both lanes:
@@ -183,6 +200,11 @@ struct EqArgs {
     float *xs;         // tile-major f32 scratch: pass 1 leaves the exciter's output here for pass 2
 };
 
+// Staging buffer: two steps of EQ_STAGE frames for the block's TPB tiles (rows
+// padded by one frame against bank conflicts); the look-back scratch aliases it
+// between the passes.  The exciter's codes are a static 8 KB beside it (three
+// blocks per CU; an unpadded XOR-swizzled stage with the codes in its place, four
+// blocks per CU, measured slower: eq 0.234 against 0.173 ms).
 template <int CH>
 constexpr int eq_stage_bytes() {
     return 2 * (LB_THREADS / CH) * (EQ_STAGE + 1) * CH * (int)sizeof(float);
@@ -197,7 +219,8 @@ constexpr int eq_lds_bytes() {
 // threads read one tile's 128 contiguous bytes), double-buffered so the next
 // stage's loads are in flight while lanes run the recurrence.
 template <int NS, int CH, bool P2, bool I16>
-__device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, double (&z)[NS][2], float *stage) {
+__device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, double (&z)[NS][2], float *stage,
+                        const uint32_t *codes) {
     constexpr int TPB = LB_THREADS / CH;
     constexpr int ROW = (EQ_STAGE + 1) * CH;       // floats per staged tile row (padded)
     constexpr int ITEMS = TPB * EQ_STAGE / LB_THREADS;  // frames each thread loads per step
@@ -233,6 +256,13 @@ __device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, doub
             }
         }
     };
+    // The exciter runs here, on the staged values, once per sample (its codes are LDS
+    // reads: no vector-memory wait in the per-frame loop below)
+    // The exciter runs in the per-frame loop below: tanhf fills the issue slots the
+    // f64 chain leaves, and its correction codes are LDS reads, so no vector-memory
+    // wait sits in that loop (one would drain the staging prefetch at every frame).
+    // Only an incomplete code table (no known input) gathers from the full table
+    // there instead.
     auto store = [&](int buf) {
 #pragma unroll
         for (int r = 0; r < ITEMS; ++r) {
@@ -256,7 +286,7 @@ __device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, doub
             const int n = step * EQ_STAGE + j;
             if (n >= len) break;
             float x = row[j * CH + c];
-            if (a.sat.on) x = saturate(x, a.sat);
+            if (a.sat.on) x = codes ? saturate_corr(x, a.sat, codes) : saturate(x, a.sat);
             if (!P2) a.xs[((int64_t)n * a.G + g0 + t) * CH + c] = x;  // pass 2 reads it back coalesced
             double y = (double)x;
 #pragma unroll
@@ -337,6 +367,7 @@ __global__ void __launch_bounds__(LB_THREADS, 4) eq_kernel(EqArgs a, LbArgs lb, 
     constexpr int TPB = LB_THREADS / CH;
     constexpr int DIM = 2 * NS;
     __shared__ int ticket_slot;
+    __shared__ uint32_t codes_lds[SAT_CORR_WORDS];  // the exciter's correction codes for pass 1
     const int blk = lb_ticket(lb, &ticket_slot);
     const int tid = threadIdx.x;
     const int c = CH == 2 ? (tid & 1) : 0;
@@ -358,7 +389,12 @@ __global__ void __launch_bounds__(LB_THREADS, 4) eq_kernel(EqArgs a, LbArgs lb, 
     // 0.166 ms); pass 2 takes the uniform-row path on full blocks.
     const bool full = (g0 + TPB) * a.T <= a.N_proc;
 #ifndef MM_ABL_EQ_NOP1  // (ablation builds: timing only)
-    eq_pass<NS, CH, false, I16>(a, g0, t, c, len, zs, stage);
+    // the exciter's correction codes into LDS (ordered before their reads by eq_pass's
+    // first barrier)
+    const bool codes_on = a.sat.on && a.sat.corr;
+    if (codes_on)
+        for (int i = tid; i < SAT_CORR_WORDS; i += LB_THREADS) codes_lds[i] = a.sat.corr[i];
+    eq_pass<NS, CH, false, I16>(a, g0, t, c, len, zs, stage, codes_on ? codes_lds : nullptr);
 #endif
     double z[DIM], s[DIM], rst[DIM];
 #pragma unroll
@@ -618,11 +654,12 @@ struct KwArgs {
     const int64_t *trk_tile0;  // [n_trk] ascending
     const int64_t *trk_end;    // [n_trk] timeline frame
     // exact block energies (kw_blocks_kernel): pass 2 writes the f32 square of every
-    // K-weighted frame here instead of segment partials, tile-major like the mix
-    // (frame n of tile g at n * sq_stride + g: coalesced stores) with the row stride
-    // a multiple of 4 (16-byte loads along the tiles)
+    // K-weighted frame here instead of segment partials, in frame order with every
+    // mix tile padded to sq_tp = Tt rounded up to 4 frames (frame n of mix tile g at
+    // g * sq_tp + n): a lane stores 16 bytes every 4 frames, and a loudness chunk's
+    // frames are ~37 contiguous runs the block sums load 16 bytes at a time
     float *sq;
-    int64_t sq_stride;
+    int sq_tp;
 };
 
 // pyloudnorm Meter (AME:213-218): mono = f32 mean(L,R) (== (L+R)/65536 exactly),
@@ -641,8 +678,9 @@ __device__ __forceinline__ void kw_pass(const KwArgs &a, int64_t g, int len, dou
     const short2 *mix = reinterpret_cast<const short2 *>(a.mix) + (g - gt * a.sub) * a.T * a.Gt + gt;
     const int64_t Gt = a.Gt;
     int64_t pf = g * a.T;
-    float *sq = SQ ? a.sq + gt + (g - gt * a.sub) * a.T * a.sq_stride : nullptr;
-    const int64_t sqs = SQ ? a.sq_stride : 0;
+    float *sq = SQ ? a.sq + gt * a.sq_tp + (g - gt * a.sub) * a.T : nullptr;  // (sub-tile starts: multiples of T)
+    float4 sq4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    int nsq = 0;
     stream<8, MM_KW_NB, short2>(
         len, [&](int i) { return mix[(int64_t)min(i, len - 1) * Gt]; },
         [&](short2 q) {
@@ -651,8 +689,22 @@ __device__ __forceinline__ void kw_pass(const KwArgs &a, int64_t g, int len, dou
             if constexpr (P2 && SQ) {
                 const float y1f = (float)df2t_lfilter((double)m, z[0][0], z[0][1], a.sos[0]);
                 const float y2f = (float)df2t_lfilter((double)y1f, z[1][0], z[1][1], a.sos[1]);
-                *sq = __fmul_rn(y2f, y2f);
-                sq += sqs;
+                // 16-byte stores when the tile starts 16-byte aligned (the chain: sub = 1,
+                // sq_tp % 4 == 0), else one word per frame
+                const float v = __fmul_rn(y2f, y2f);
+                if (a.sub == 1) {  // (a shift register: no per-frame component select)
+                    sq4.x = sq4.y;
+                    sq4.y = sq4.z;
+                    sq4.z = sq4.w;
+                    sq4.w = v;
+                    if (++nsq == 4) {
+                        *reinterpret_cast<float4 *>(sq) = sq4;
+                        sq += 4;
+                        nsq = 0;
+                    }
+                } else {
+                    *sq++ = v;
+                }
             } else {
                 const double y1 = df2t((double)m, z[0][0], z[0][1], a.sos[0]);
                 const float y1f = (float)y1;
@@ -666,6 +718,11 @@ __device__ __forceinline__ void kw_pass(const KwArgs &a, int64_t g, int len, dou
             }
             ++pf;
         });
+    if constexpr (P2 && SQ) {  // the tile's last T % 4 frames: the newest nsq entries of the register
+        if (nsq == 1) sq[0] = sq4.w;
+        if (nsq == 2) sq[0] = sq4.z, sq[1] = sq4.w;
+        if (nsq == 3) sq[0] = sq4.y, sq[1] = sq4.z, sq[2] = sq4.w;
+    }
 }
 
 template <bool SQ>

@@ -40,6 +40,7 @@ struct KStat {
 
 struct mm_ctx {
     int device = 0;
+    int n_cus = 256;  // compute units of the device (persistent launches)
     hipStream_t stream = nullptr;
     char err[512] = {0};
     std::map<std::string, DevBuf> bufs;
@@ -72,8 +73,9 @@ struct mm_ctx {
     int64_t *seg_bounds_dev = nullptr;
     // exact block energies (kw_blocks_kernel): per block its first frame and program
     int64_t *kb_lo = nullptr;
-    int32_t *kb_prog_of = nullptr, *kb_prog = nullptr;
+    int32_t *kb_n = nullptr, *kb_prog_of = nullptr, *kb_prog = nullptr;
     std::vector<int64_t> kb_cache;      // block geometry the programs on the device were built for
+    int kb_nvals = 0, kb_pints = 0;     // the largest program's values and ints (kw_blocks' LDS)
     // timing
     bool timing = false;
     std::vector<PendingEvent> pending;
@@ -86,6 +88,8 @@ struct mm_ctx {
     // host tables already resident on the device
     uint64_t lut_key[3] = {0, 0, 0};  // content keys of the band tables on the device (0: none)
     uint64_t sat_key = 0;             // content key of the exciter table on the device (0: none)
+    bool sat_codes = false;           // its correction codes are complete (no entry needs the table)
+    uint32_t sat_code_m = 0;          // the code of k = -32768
     std::map<std::string, std::vector<double>> mats_cache;
     // pinned block the chain's results are copied into (one sync per chain)
     char *rb = nullptr;
@@ -683,14 +687,26 @@ static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
         float *tab;
         uint32_t *corr;
         RET(get_buf(c, "sat_tab", 65536, &tab));
-        RET(get_buf(c, "sat_corr", 4096, &corr));
+        RET(get_buf(c, "sat_corr", SAT_CORR_WORDS, &corr));
         ea.sat.tab = tab;
-        if (j->sat_key == 0 || c->sat_key != j->sat_key) {
+        if (j->sat_key == 0 || c->sat_key != j->sat_key) {  // once per table: build the codes, count exceptions
+            unsigned *exc;
+            RET(get_buf(c, "sat_exc", 2, &exc));
             HIPCHK(c, hipMemcpyAsync(tab, j->sat_table, 65536 * sizeof(float), hipMemcpyHostToDevice, c->stream));
-            RET(launch(c, "sat_corr", sat_corr_kernel, dim3(16), dim3(256), 0, ea.sat, corr));
+            HIPCHK(c, hipMemsetAsync(exc, 0, 2 * sizeof(unsigned), c->stream));
+            RET(launch(c, "sat_corr", sat_corr_kernel, dim3((SAT_CORR_WORDS + 255) / 256), dim3(256), 0, ea.sat, corr,
+                       exc));
+            unsigned e2[2] = {1, 0};
+            HIPCHK(c, hipMemcpyAsync(e2, exc, 2 * sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            c->sat_codes = e2[0] == 0;
+            c->sat_code_m = e2[1];
             c->sat_key = j->sat_key;
         }
-        if (!getenv("MM_SAT_GATHER")) ea.sat.corr = corr;  // (A/B: a full-table gather per sample)
+        // codes when complete (else, and for A/B: a full-table gather per sample)
+        ea.sat.code_m = c->sat_code_m;
+        if (c->sat_codes && !getenv("MM_SAT_GATHER")) ea.sat.corr = corr;
+        if (getenv("MM_SAT_TANHF")) ea.sat.tab = nullptr, ea.sat.corr = nullptr;  // (A/B: round 5's tanhf alone)
     }
     ea.width = j->width;
     ea.width_on = j->width_on && ch == 2;
@@ -892,29 +908,40 @@ static int kb_upload(mm_ctx *c, const std::vector<int64_t> &lo, const std::vecto
     const size_t nb = lo.size();
     RET(get_buf(c, "kb_lo", std::max<size_t>(nb, 1), &c->kb_lo));
     RET(get_buf(c, "kb_prog_of", std::max<size_t>(nb, 1), &c->kb_prog_of));
+    RET(get_buf(c, "kb_n", std::max<size_t>(nb, 1), &c->kb_n));
     if (key == c->kb_cache && c->kb_prog) return MM_OK;
     std::map<int64_t, int32_t> at;
-    std::vector<int32_t> prog, of(nb);
+    std::vector<int32_t> prog, of(nb), n32(nb);
+    int nvals = 1, pints = 4;
     for (size_t b = 0; b < nb; ++b) {
         if (n[b] < 0 || n[b] > 16 * KB_CHUNK) return set_err(c, MM_ERR_ARG, "loudness block of %lld frames", (long long)n[b]);
         auto it = at.find(n[b]);
         if (it == at.end()) {
             const int32_t o = (int32_t)prog.size();
             pw_build(n[b], prog);
-            if (prog[o] + prog[o + 1] > KB_VMAX) return set_err(c, MM_ERR_ARG, "loudness block program too large");
+            if (prog[o] + prog[o + 1] > KB_VMAX || (int64_t)prog.size() - o > KB_PMAX)
+                return set_err(c, MM_ERR_ARG, "loudness block program too large");
+            while (prog.size() % 4) prog.push_back(0);  // (16-byte aligned programs: int4 copies)
+            nvals = std::max(nvals, prog[o] + prog[o + 1]);
+            pints = std::max(pints, (int)(prog.size() - o));
             it = at.emplace(n[b], o).first;
         }
         of[b] = it->second;
+        n32[b] = (int32_t)n[b];
     }
     c->kb_prog = nullptr;  // (get_buf may move it: re-fetched below)
-    RET(get_buf(c, "kb_prog", std::max<size_t>(prog.size(), 1), &c->kb_prog));
+    prog.resize(prog.size() + pints, 0);  // every block copies the largest program's length
+    RET(get_buf(c, "kb_prog", prog.size(), &c->kb_prog));
     if (nb) {
         HIPCHK(c, hipMemcpyAsync(c->kb_lo, lo.data(), nb * 8, hipMemcpyHostToDevice, c->stream));
         HIPCHK(c, hipMemcpyAsync(c->kb_prog_of, of.data(), nb * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->kb_n, n32.data(), nb * 4, hipMemcpyHostToDevice, c->stream));
         HIPCHK(c, hipMemcpyAsync(c->kb_prog, prog.data(), prog.size() * 4, hipMemcpyHostToDevice, c->stream));
     }
     HIPCHK(c, hipStreamSynchronize(c->stream));  // host vectors are transient
     c->kb_cache = key;
+    c->kb_nvals = nvals;
+    c->kb_pints = pints;
     return MM_OK;
 }
 
@@ -976,11 +1003,10 @@ static int kweight_exact(mm_ctx *c, const mm_job &j0, int64_t frames, int n_trk,
     const int64_t GS = G * sub;
     float *sq;
     double *zl;
-    const int64_t stride = (G + 3) / 4 * 4;  // tile-major rows, 16-byte aligned (kw_blocks' loads)
-    const int Tt = j0.tile;
-    if ((int64_t)Tt * ((KB_CHUNK / Tt + 3) / 4 + 2) > (int64_t)KB_LD * KB_THREADS)
-        return set_err(c, MM_ERR_ARG, "tile of %d frames too long for the loudness block loads", Tt);
-    RET(get_buf(c, "kw_sq", (size_t)(Tt * stride), &sq));
+    const int Tt = j0.tile, TP = (Tt + 3) / 4 * 4;  // padded tile stride (16-byte stores and loads)
+    if (((KB_CHUNK - 1) / Tt + 2) * (TP / 4) > KB_LD * KB_THREADS)
+        return set_err(c, MM_ERR_ARG, "tile of %d frames: the loudness block loads do not cover a chunk", Tt);
+    RET(get_buf(c, "kw_sq", (size_t)(G * TP), &sq));
     RET(get_buf(c, "gate_zl", (size_t)std::max<int64_t>(2 * nb, 2), &zl));
     LbArgs lb{};
     RET(upload_tables(c, "kweight", j0.kweight, lb));
@@ -1000,21 +1026,28 @@ static int kweight_exact(mm_ctx *c, const mm_job &j0, int64_t frames, int n_trk,
     ka.trk_tile0 = trk_tile0;
     ka.trk_end = trk_end;
     ka.sq = sq;
-    ka.sq_stride = stride;
+    ka.sq_tp = TP;
     RET(launch(c, "kweight", kweight_kernel<true>, dim3(nblk), dim3(LB_THREADS), lb_lds_bytes<4, 1>(), ka, lb));
     if (nb > 0) {
         KbArgs kb{};
         kb.sq = sq;
-        kb.sq_stride = stride;
         kb.T = Tt;
+        kb.TP = TP;
         kb.n_blocks = nb;
         kb.blk_lo = c->kb_lo;
         kb.blk_prog = c->kb_prog_of;
+        kb.blk_n = c->kb_n;
         kb.prog = c->kb_prog;
         kb.scale = (float)j0.block_scale;  // Python float * np.float32: the constant rounded to f32 (NEP 50)
         kb.zl = zl;
-        const unsigned grid = (unsigned)((nb + 7) / 8 * 8);  // a multiple of 8 (the XCD-aware block mapping)
-        RET(launch(c, "kw_blocks", kw_blocks_kernel, dim3(grid), dim3(KB_THREADS), 0, kb));
+        kb.stage_floats = kb_pad(KB_CHUNK);
+        kb.nvals = 2 * c->kb_nvals;  // (two value buffers)
+        kb.pints = c->kb_pints;
+        const size_t lds = (size_t)kb_lds_bytes(kb.stage_floats, kb.nvals, kb.pints);
+        // persistent: as many workgroups as fit at once (a multiple of 8: the XCD-aware block mapping)
+        const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(KB_RING == 1 ? 4 : 2, (160 * 1024) / (int64_t)(lds + 64)));  // (and VGPRs)
+        const unsigned grid = (unsigned)std::min<int64_t>((nb + 7) / 8 * 8, (int64_t)c->n_cus * per_cu / 8 * 8);
+        RET(launch(c, "kw_blocks", kw_blocks_kernel, dim3(std::max(grid, 8u)), dim3(KB_THREADS), lds, kb));
     }
     *zl_out = zl;
     return MM_OK;
@@ -1577,6 +1610,9 @@ int mm_create(int device, mm_ctx **out) {
         delete c;
         return MM_ERR_HIP;
     }
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
+        c->n_cus = ncu;
     *out = c;
     return MM_OK;
 }

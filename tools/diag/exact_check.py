@@ -43,6 +43,8 @@ def oracle_mix(pcm, rate, params):
 
 def one(name, pcm, rate, params):
     mix, rmix = staged_mix(pcm, rate, params), oracle_mix(pcm, rate, params)
+    nm = min(len(mix), len(rmix))
+    mix, rmix = mix[:nm], rmix[:nm]
     out, info = master_pcm(pcm, rate, params)
     ref, L = mo.master(pcm, rate, params, return_loudness=True)
     print(f"{name}: mix exact {np.mean(mix == rmix):.7f}  dL {info['loudness'] - L:+.3e} (L {L:.12f})  "

@@ -6,6 +6,7 @@
 #   bash tools/gpu.sh iter [variants...]              C2 / C2 P_HOT bench lines with the
 #        per-kernel split; a variant is "ENV=x" (library env knob), "tune:NAME=V"
 #        (bench tune) or "lib:<path.so>" (an ablation build from tools/build_var.sh)
+#   bash tools/gpu.sh c2 [variants...]                C2 lines only (variants as in iter)
 #   bash tools/gpu.sh configs [C3 C4 C5 C1 ...]       bench lines of the other workloads
 #   bash tools/gpu.sh measure <round> [notest] [workloads...]  end-of-round measurement: tests, smoke,
 #        per workload the rocprofv3 trace + PMC passes (tools/pmc.sh ->
@@ -45,6 +46,20 @@ mode_iter() {
       lib:*)  bench_line C2_v$i "MM_LIB=$PWD/${v#lib:}" --workload C2 && \
               bench_line C2hot_v$i "MM_LIB=$PWD/${v#lib:}" --workload C2 --params hot || return 1 ;;
       *)      bench_line C2_v$i "$v" --workload C2 && bench_line C2hot_v$i "$v" --workload C2 --params hot || return 1 ;;
+    esac
+    echo "  (v$i = $v)"
+  done
+}
+
+mode_c2() {  # C2 lines only (P_FULL): the product, then each variant (as in iter)
+  bench_line C2 - --workload C2 || return 1
+  local i=0 v
+  for v in "$@"; do
+    i=$((i + 1))
+    case $v in
+      tune:*) bench_line C2_v$i - --workload C2 --tune ${v#tune:} || return 1 ;;
+      lib:*)  bench_line C2_v$i "MM_LIB=$PWD/${v#lib:}" --workload C2 || return 1 ;;
+      *)      bench_line C2_v$i "$v" --workload C2 || return 1 ;;
     esac
     echo "  (v$i = $v)"
   done
