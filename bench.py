@@ -64,7 +64,7 @@ import numpy as np  # noqa: E402
 METRIC = "stereo frames/sec through full mastering chain, 44.1 kHz f32; 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 CHAIN_BYTES_PER_FRAME = 16  # f32 L,R in + f32 L,R out
-PROFILE_ROUND = "r05"  # profiles/<round>_<workload>_pmc_summary.json carry the PMC traffic
+PROFILE_ROUND = "r06"  # profiles/<round>_<workload>_pmc_summary.json carry the PMC traffic
 P_FULL = {"bass_boost": 4.0, "mid_cut": 3.0, "presence_boost": 1.0, "treble_boost": 3.0,
           "saturation": 30, "width": 1.3, "multiband": True, "lufs": -14.0}
 P_HOT = dict(P_FULL, low_thresh=-16.0, mid_thresh=-21.0, high_thresh=-27.0)
@@ -119,7 +119,8 @@ def intermediate_bytes(kernel, n, g, active, walked_per_launch):
         "comp_pass0": 8 * active,             # M of every active band-frame
         "comp_fix": 8 * walked_per_launch,    # M of the re-walked frames
         "comp_apply": 8 * active + 12 * n + 4 * n,  # M of the active frames, bands in; mix out
-        "kweight": 4 * n,                     # mix in
+        "kweight": 4 * n + 4 * n,             # mix in; f32 squares out (exact block energies)
+        "kw_blocks": 16 * n,                  # the squares, once per overlapping 0.4 s block (4x)
         "seg_reduce": g * 24,
         "gate": 0,
         "finalize": 4 * n + 8 * n,            # mix in; f32 L,R out
@@ -349,6 +350,35 @@ def valu_floor(prof, n_frames, ms_step):
             "scope": "SQ_INSTS_VALU x 64 x launches per step / frames per step, summed over the chain's kernels"}
 
 
+# Arithmetic the exact recurrences themselves need, per stereo frame (DESIGN.md §4's
+# column): fixed per frame, or per active / re-walked band-frame.
+NEEDED_OPS_PER_FRAME = {"eq": 120, "xover": 122, "comp_rms": 39, "comp_apply": 45, "kweight": 22, "finalize": 10,
+                        "kw_blocks": 4}  # (kw_blocks: numpy's f32 adds, 4 overlapping 0.4 s blocks per frame)
+NEEDED_OPS_PER_ACTIVE = {"comp_describe": 16, "comp_pass0": 8}  # per active band-frame
+NEEDED_OPS_PER_REWALKED = {"comp_fix": 8}  # per re-walked band-frame
+
+
+def needed_floor(per_kernel_ms, n_frames, active, walked, ms_step):
+    """The time the chip needs for the arithmetic the exact algorithm needs (not the
+    instructions issued: no addressing, conversions, divergence or two-pass IIR
+    overhead) at 39.3 T lane-ops/s, and the HBM fraction the 16 B/frame roofline
+    would reach at that floor: the ceiling of an exact f64 implementation."""
+    per = {k: float(v) for k, v in NEEDED_OPS_PER_FRAME.items() if k in per_kernel_ms}
+    for k, v in NEEDED_OPS_PER_ACTIVE.items():
+        if k in per_kernel_ms:
+            per[k] = v * active / n_frames
+    for k, v in NEEDED_OPS_PER_REWALKED.items():
+        if k in per_kernel_ms:
+            per[k] = v * walked / n_frames
+    tot = sum(per.values())
+    floor_ms = tot * n_frames / LANE_OPS_PEAK * 1e3
+    return {"ops_per_frame": tot, "needed_floor_ms": floor_ms, "frac": floor_ms / ms_step,
+            "hbm_frac_at_needed_floor": CHAIN_BYTES_PER_FRAME * n_frames / (floor_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+            "per_kernel_ops_per_frame": {k: round(v, 2) for k, v in per.items()},
+            "scope": "f64/f32 operations the exact recurrences need per stereo frame (active and re-walked "
+                     "band-frames from the run), at 1024 SIMDs x 16 lanes x 2.4 GHz"}
+
+
 def profile_summary(tag):
     path = os.path.join(ROOT, "profiles", f"{tag}_pmc_summary.json")
     try:
@@ -551,6 +581,10 @@ def main(argv=None):
                 dom_traffic = k.get("bytes_per_launch")
                 valu = valu_ceiling(prof, dom)
                 vfloor = valu_floor(prof, n_frames, ms_step)
+        if vfloor is None:
+            vfloor = {}
+        vfloor["needed"] = needed_floor({k: v[0] for k, v in per.items()}, n_frames, active, walked, ms_step)
+        vfloor["needed_floor_ms"] = vfloor["needed"]["needed_floor_ms"]
         line = {
             "metric": METRIC, "value": value, "unit": "stereo frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,

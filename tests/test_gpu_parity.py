@@ -24,17 +24,20 @@ def rms_diff(a, b):
     return float(np.sqrt(np.mean(((a.astype(np.float64) - b.astype(np.float64)) / 32768.0) ** 2)))
 
 
-# Identical int16 output samples, tied to what is measured (round 3, `pytest -m gpu`
-# summary, profiles/r03_final_gpu_pytest.log): 99.9457-99.992 % on every full-chain
-# case but loud_sat100 (99.871 %, its own floor), the lowest being
-# test_batch_device_resident at 44.1 kHz (0.9994570).  The differences come from
-# numpy's float32 tanh (not correctly rounded), carried through the
-# compressor; with the exciter off the pre-gain mix is 100 % identical
-# (test_mix_bit_exact_without_tanh).  The floor allows twice the worst measured
-# mismatch rate (2 x 5.43e-4), so a regression from 99.95 % to 99.8 % fails.
-MIN_EXACT = 0.9989
-
-
+# Identical int16 output samples (round 6, profiles/r06_gpu_pytest.log).  The
+# exciter reads numpy's own float32 values on the int16 grid (design.saturation_table)
+# and the loudness block energies follow numpy's float32 reduction order
+# (kw_blocks_kernel), so every reference golden and every oracle comparison of the
+# single-track path is bit-identical: GOLDEN_EXACT.  The one remaining source of
+# differences is the K-weighting carry: the look-back composes tile maps, so a
+# tile's carry-in can differ from lfilter's sequential state in its last bits and,
+# rarely, flip an f32 filter output next to a rounding boundary; that moves a block
+# energy by one f32 step and L by ~1e-9 LU, and the gain then moves a few f32
+# products across an int16 boundary (measured: >= 0.99993 on the cases it touches:
+# the fused batches, 44056 Hz).  The time-sharded path (C4) keeps f64 segment
+# energies (an all-reduce of segments; its block sums are not numpy's): tolerance.
+GOLDEN_EXACT = 1.0
+MIN_EXACT = 0.9998
 def _check(out, info, ref, L, min_exact=MIN_EXACT):
     """North-star tolerances, plus the identical-sample floor; records the
     fraction (printed at the end of the run)."""
@@ -62,9 +65,7 @@ def test_golden(path):
     st = json.loads(str(d["settings"]))
     out, info = master_pcm(d["pcm"], int(d["rate"]), st)
     L = float(d["loudness"])
-    # saturation 100 %: the exciter's tanh decides every sample (measured 99.871 %)
-    floor = 0.997 if os.path.basename(path) == "loud_sat100.npz" else MIN_EXACT
-    _check(out, info, d["out"], None if np.isnan(L) else L, floor)
+    _check(out, info, d["out"], None if np.isnan(L) else L, GOLDEN_EXACT)
 
 
 @pytest.mark.parametrize("seconds,params,track", [(35, P_FULL, 1), (12, P_HOT, 2)])
@@ -74,7 +75,20 @@ def test_vs_oracle(oracle, seconds, params, track):
     pcm = pink_noise_pcm16(seconds * 44100, 44100, 2, track)
     out, info = master_pcm(pcm, 44100, params)
     ref, L = oracle.master(pcm, 44100, params, return_loudness=True)
-    _check(out, info, ref, L)
+    _check(out, info, ref, L, GOLDEN_EXACT)  # (measured bit-identical)
+
+
+@pytest.mark.parametrize("saturation", [10, 55.5, 100])
+def test_exciter_every_grid_input(saturation):
+    """apply_saturation's operator on every int16-grid input equals numpy's value
+    (design.saturation_table) for all 65 536 inputs.  (The chain's EQ kernel instead
+    corrects its tanhf with 2-bit codes built from that table by sat_corr_kernel;
+    test_mix_with_exciter and the goldens check that path end to end.)"""
+    from mastering_amd import design, ops
+    tab, _ = design.saturation_table(saturation)
+    x = np.arange(-32768, 32768, dtype=np.int32).astype(np.int16).astype(np.float32) / 32768
+    y = ops.apply_saturation(x, saturation)
+    assert np.array_equal(y, tab)
 
 
 def _staged_mix(pcm, params):
@@ -118,13 +132,14 @@ def test_mix_bit_exact_without_tanh(oracle):
 
 
 def test_mix_with_exciter(oracle):
-    """With the exciter on, numpy's float32 tanh is not correctly rounded (1 ulp apart from
-    the GPU's tanhf on ~30 % of samples), which flips a few int16 truncations: tolerance."""
+    """With the exciter on: numpy's float32 tanh is not correctly rounded, so the device
+    corrects its tanhf by a 2-bit code per int16-grid input onto numpy's own values
+    (design.saturation_table, sat_corr_kernel): the pre-gain mix is bit-identical."""
     from mastering_amd.synth import pink_noise_pcm16
     pcm = pink_noise_pcm16(31 * 44100, 44100, 2, 5)
     mix, ref = _staged_mix(pcm, P_HOT), _oracle_mix(oracle, pcm, P_HOT)
     record_exact(np.mean(mix == ref), "mix")
-    assert rms_diff(mix, ref) <= RMS_TOL and np.mean(mix == ref) >= 0.9998  # measured 99.989 %
+    assert np.array_equal(mix, ref), np.mean(mix == ref)
 
 
 class _ThreadCollectives:
