@@ -200,15 +200,20 @@ __global__ void __launch_bounds__(KB_THREADS) kw_blocks_kernel(KbArgs a) {
             const int l0 = chunk_leaf[c], l1 = chunk_leaf[c + 1];
             // this chunk from its ring buffer into LDS, then that buffer takes the stream's
             // chunk three ahead (static buffer indices: no register array indexing)
+#ifndef MM_KB_NOCOPY  // (ablation builds: timing only)
             if (KB_RING == 1 || ring == 0) copy(std::integral_constant<int, 0>{});
             else if (KB_RING == 2 || ring == 1) copy(std::integral_constant<int, 1 % KB_RING>{});
             else copy(std::integral_constant<int, 2 % KB_RING>{});
+#endif
             __syncthreads();
             if (KB_RING == 1 || ring == 0) issue(std::integral_constant<int, 0>{});
             else if (KB_RING == 2 || ring == 1) issue(std::integral_constant<int, 1 % KB_RING>{});
             else issue(std::integral_constant<int, 2 % KB_RING>{});
             ring = ring == KB_RING - 1 ? 0 : ring + 1;
             const int q = tid & 7;  // accumulator q of the leaf (eight lanes per leaf)
+#ifdef MM_KB_NOLEAF  // (ablation builds: timing only)
+            if (l1 < 0)
+#endif
             for (int li = l0 + (tid >> 3); li < l1; li += KB_THREADS / 8) {
                 const int off = loff[li] - c * KB_CHUNK, len = llen[li];
                 float res;
@@ -241,10 +246,12 @@ __global__ void __launch_bounds__(KB_THREADS) kw_blocks_kernel(KbArgs a) {
             }
             __syncthreads();  // (the next chunk overwrites el; the levels read V)
         }
+#ifndef MM_KB_NOLEVEL  // (ablation builds: timing only)
         for (int L = 0; L < nlev; ++L) {
             for (int k = lvl[L] + tid; k < lvl[L + 1]; k += KB_THREADS) V[nl + k] = __fadd_rn(V[na[k]], V[nb[k]]);
             __syncthreads();
         }
+#endif
         if (tid == 0) {
             const float sm = root < 0 ? 0.0f : V[root];
             const double z = (double)__fmul_rn(a.scale, sm);

@@ -123,6 +123,16 @@ __global__ void __launch_bounds__(256) sat_corr_kernel(SatArgs s, uint32_t *corr
     }
 }
 
+// The exciter as a pointwise pre-pass (decoded input -> f32), for the EQ kernel when
+// the correction codes are incomplete: the full table per grid sample, tanhf off it.
+__global__ void __launch_bounds__(256) sat_pre_kernel(const float *in, const int16_t *in16, int64_t n, SatArgs s,
+                                                      float *out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float x = in16 ? (float)in16[i] * (1.0f / 32768.0f) : in[i];
+    out[i] = saturate(x, s);
+}
+
 // apply_stereo_width (AME:136-144) on a lane pair, one formula for both lanes:
 // with y this lane's sample and o its partner's, the left lane's mid + side and
 // the right lane's mid - side are both RN(RN(y + o)/2 + RN(RN(y - o) * (w/2)))
@@ -261,8 +271,8 @@ __device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, doub
     // The exciter runs in the per-frame loop below: tanhf fills the issue slots the
     // f64 chain leaves, and its correction codes are LDS reads, so no vector-memory
     // wait sits in that loop (one would drain the staging prefetch at every frame).
-    // Only an incomplete code table (no known input) gathers from the full table
-    // there instead.
+    // An incomplete code table (no known input) is applied by sat_pre_kernel before
+    // this kernel instead (the EQ then runs with the exciter off).
     auto store = [&](int buf) {
 #pragma unroll
         for (int r = 0; r < ITEMS; ++r) {
@@ -286,7 +296,9 @@ __device__ void eq_pass(const EqArgs &a, int64_t g0, int t, int c, int len, doub
             const int n = step * EQ_STAGE + j;
             if (n >= len) break;
             float x = row[j * CH + c];
-            if (a.sat.on) x = codes ? saturate_corr(x, a.sat, codes) : saturate(x, a.sat);
+            // (no global load may sit in this loop, even unexecuted: the compiler's waits
+            // would drain the staging prefetch; the full-table case runs as a pre-pass)
+            if (a.sat.on) x = codes ? saturate_corr(x, a.sat, codes) : saturate_dev(x, a.sat);
             if (!P2) a.xs[((int64_t)n * a.G + g0 + t) * CH + c] = x;  // pass 2 reads it back coalesced
             double y = (double)x;
 #pragma unroll

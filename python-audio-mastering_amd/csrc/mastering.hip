@@ -707,6 +707,19 @@ static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
         ea.sat.code_m = c->sat_code_m;
         if (c->sat_codes && !getenv("MM_SAT_GATHER")) ea.sat.corr = corr;
         if (getenv("MM_SAT_TANHF")) ea.sat.tab = nullptr, ea.sat.corr = nullptr;  // (A/B: round 5's tanhf alone)
+        if (ea.sat.tab && !ea.sat.corr && j->eq.nsec > 0 && N > 0) {
+            // the EQ kernel takes the exciter only as tanhf + codes: the table case runs
+            // as a pointwise pre-pass into a decoded f32 input, and the EQ without it
+            const int64_t n = j->frames_in * ch;
+            float *pre;
+            RET(get_buf(c, "sat_pre", (size_t)std::max<int64_t>(n, 1), &pre));
+            if (n > 0)
+                RET(launch(c, "sat_pre", sat_pre_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, ea.in, ea.in16, n,
+                           ea.sat, pre));
+            ea.in = pre;
+            ea.in16 = nullptr;
+            ea.sat.on = 0;
+        }
     }
     ea.width = j->width;
     ea.width_on = j->width_on && ch == 2;

@@ -335,3 +335,18 @@ def test_sweep_queue_across_settings_on_one_context():
         assert res.loudness == rres.loudness
         assert res.comp_iters == rres.comp_iters
     shared.close()
+
+
+@pytest.mark.parametrize("name", ["full_4s.npz", "loud_sat100.npz", "mono_hot_2s.npz"])
+def test_exciter_table_prepass(name, monkeypatch):
+    """The exciter's other exact path: when the correction codes are incomplete (an
+    entry more than one f32 step from numpy's value; MM_SAT_GATHER forces it) the
+    full table is applied by a pointwise pre-pass (sat_pre_kernel) and the EQ runs
+    with the exciter off: still bit-identical to the reference."""
+    from mastering_amd import master_pcm
+    monkeypatch.setenv("MM_SAT_GATHER", "1")
+    d = np.load(os.path.join(GOLDEN, name))
+    st = json.loads(str(d["settings"]))
+    out, info = master_pcm(d["pcm"], int(d["rate"]), st)
+    L = float(d["loudness"])
+    _check(out, info, d["out"], None if np.isnan(L) else L, GOLDEN_EXACT)
