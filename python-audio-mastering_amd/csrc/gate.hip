@@ -82,9 +82,10 @@ __host__ __device__ constexpr int kb_lds_bytes(int stage_floats, int nvals, int 
 // x per + w/8, + grid/8, ... of its XCD's contiguous range (neighbouring blocks'
 // windows overlap 3/4: the re-reads hit that XCD's L2).  The blocks' chunks
 // (8192 frames, numpy's buffers) form one stream over all the workgroup's blocks
-// with KB_RING chunks' 16-byte loads in flight (a ring of register buffers).  Per chunk the frames are copied to
-// LDS in frame order (8 words of padding per 128 frames: kb_pad); eight lanes per
-// leaf run numpy's eight accumulators; per block the
+// with KB_RING chunks' 16-byte loads in flight (a ring of register buffers).  Per
+// chunk the tiles' padded runs are copied to LDS as they lie in memory (a plain
+// 16-byte copy); eight lanes per leaf run numpy's eight accumulators, walking the
+// frames' word addresses; per block the
 // program's levels combine the leaves in numpy's order.  A block's program (one
 // per block length) stays in LDS while the next block has the same.
 #ifndef MM_KB_RING
@@ -103,15 +104,12 @@ __global__ void __launch_bounds__(KB_THREADS) kw_blocks_kernel(KbArgs a) {
     const int xcd = (int)(blockIdx.x % 8), nslot = (int)(gridDim.x / 8);
     const int64_t jb = xcd * per + blockIdx.x / 8, je = min((int64_t)(xcd + 1) * per, nbk);
     if (jb >= je) return;  // (workgroup-uniform)
-    const int T = a.T, Q4 = a.TP / 4;  // frames per tile, 16-byte quads per padded tile
+    const int T = a.T, TP = a.TP, Q4 = a.TP / 4;  // frames per tile, padded tile stride, its 16-byte quads
     const float4 *sq4 = reinterpret_cast<const float4 *>(a.sq);
+    float4 *el4 = reinterpret_cast<float4 *>(el);
     if (tid == 0) kb_prog_cur = -1;
-    // a thread's (tile, quad) of its first load in a chunk and the step between its loads
-    const int t_0 = tid / Q4, k_0 = tid - (tid / Q4) * Q4;
-    const int dt = KB_THREADS / Q4, dk = KB_THREADS - (KB_THREADS / Q4) * Q4;
     float4 buf[KB_RING][KB_LD];
-    int g_i0[KB_RING], g_m[KB_RING], g_nld[KB_RING];  // per buffer: chunk index of its first tile's
-                                                      // frame 0 (<= 0), length, quads loaded
+    int g_nld[KB_RING], g_fb[KB_RING];  // per buffer: quads loaded; the chunk's first frame's row in its tile
     // the stream's next chunk: (block lj, chunk lc)
     int64_t lj = jb;
     int lc = 0;
@@ -121,6 +119,9 @@ __global__ void __launch_bounds__(KB_THREADS) kw_blocks_kernel(KbArgs a) {
         lj += nslot;
         if (lj < je) lF0 = a.blk_lo[lj], ln = a.blk_n[lj];
     }
+    // the chunk's padded tile runs [tA, tB] land in LDS as they lie in memory: quad
+    // L of the run is LDS quad L (a plain 16-byte copy); frame u of the run (u = row
+    // + T * tile) is LDS word (u / T) TP + u % T
     auto issue = [&](auto B) __attribute__((always_inline)) {  // the stream's next chunk into buffer B
         constexpr int b = decltype(B)::value;
         if (lj >= je) return;
@@ -128,21 +129,11 @@ __global__ void __launch_bounds__(KB_THREADS) kw_blocks_kernel(KbArgs a) {
         const int64_t F0 = lF0 + (int64_t)lc * KB_CHUNK;
         const int64_t tA = F0 / T;
         const int nld = (int)((F0 + m - 1) / T - tA + 1) * Q4;
-        g_i0[b] = (int)(tA * T - F0);
-        g_m[b] = m;
         g_nld[b] = nld;
+        g_fb[b] = (int)(F0 - tA * T);
         const float4 *base = sq4 + tA * Q4;
-        int t = t_0, k = k_0;
 #pragma unroll
-        for (int r = 0; r < KB_LD; ++r) {
-            buf[b][r] = base[min(t * Q4 + k, nld - 1)];  // (past the chunk: reloaded, not stored)
-            t += dt;
-            k += dk;
-            if (k >= Q4) {
-                k -= Q4;
-                ++t;
-            }
-        }
+        for (int r = 0; r < KB_LD; ++r) buf[b][r] = base[min(tid + r * KB_THREADS, nld - 1)];
         if (++lc * KB_CHUNK >= ln) {  // advance (blocks without frames have no chunks)
             lc = 0;
             for (lj += nslot; lj < je; lj += nslot) {
@@ -152,29 +143,13 @@ __global__ void __launch_bounds__(KB_THREADS) kw_blocks_kernel(KbArgs a) {
             }
         }
     };
-    auto copy = [&](auto B) __attribute__((always_inline)) {  // buffer B -> LDS in frame order
+    auto copy = [&](auto B) __attribute__((always_inline)) {  // buffer B -> LDS
         constexpr int b = decltype(B)::value;
-        const int m = g_m[b], nld = g_nld[b], i_t0 = g_i0[b];
-        int t = t_0, k = k_0;
 #pragma unroll
         for (int r = 0; r < KB_LD; ++r) {
             const float4 v = buf[b][r];
-            const int i = i_t0 + t * T + 4 * k;  // chunk index of the quad's first frame
-            const bool ld = t * Q4 + k < nld;
-            if (ld && i >= 0 && i + 3 < m && 4 * k + 3 < T) {  // (the common case: all four)
-                el[kb_pad(i)] = v.x, el[kb_pad(i + 1)] = v.y, el[kb_pad(i + 2)] = v.z, el[kb_pad(i + 3)] = v.w;
-            } else if (ld) {
-                const float e4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    if (i + e >= 0 && i + e < m && 4 * k + e < T) el[kb_pad(i + e)] = e4[e];
-            }
-            t += dt;
-            k += dk;
-            if (k >= Q4) {
-                k -= Q4;
-                ++t;
-            }
+            float *d = el + 4 * min(tid + r * KB_THREADS, g_nld[b] - 1);
+            if (tid + r * KB_THREADS < g_nld[b]) d[0] = v.x, d[1] = v.y, d[2] = v.z, d[3] = v.w;
         }
     };
     issue(std::integral_constant<int, 0>{});
@@ -198,18 +173,24 @@ __global__ void __launch_bounds__(KB_THREADS) kw_blocks_kernel(KbArgs a) {
         float *V = val + vb * ((a.nvals + 1) / 2);  // (nvals counts both buffers)
         for (int c = 0; c < nch; ++c) {
             const int l0 = chunk_leaf[c], l1 = chunk_leaf[c + 1];
-            // this chunk from its ring buffer into LDS, then that buffer takes the stream's
-            // chunk three ahead (static buffer indices: no register array indexing)
+            int fb;
 #ifndef MM_KB_NOCOPY  // (ablation builds: timing only)
-            if (KB_RING == 1 || ring == 0) copy(std::integral_constant<int, 0>{});
-            else if (KB_RING == 2 || ring == 1) copy(std::integral_constant<int, 1 % KB_RING>{});
-            else copy(std::integral_constant<int, 2 % KB_RING>{});
+            if (KB_RING == 1 || ring == 0) copy(std::integral_constant<int, 0>{}), fb = g_fb[0];
+            else if (KB_RING == 2 || ring == 1) copy(std::integral_constant<int, 1 % KB_RING>{}), fb = g_fb[1 % KB_RING];
+            else copy(std::integral_constant<int, 2 % KB_RING>{}), fb = g_fb[2 % KB_RING];
+#else
+            fb = g_fb[0];
 #endif
             __syncthreads();
             if (KB_RING == 1 || ring == 0) issue(std::integral_constant<int, 0>{});
             else if (KB_RING == 2 || ring == 1) issue(std::integral_constant<int, 1 % KB_RING>{});
             else issue(std::integral_constant<int, 2 % KB_RING>{});
             ring = ring == KB_RING - 1 ? 0 : ring + 1;
+            // chunk frame i -> LDS word
+            auto word = [&](int i) __attribute__((always_inline)) {
+                const int u = i + fb, t = u / T;
+                return t * TP + (u - t * T);
+            };
             const int q = tid & 7;  // accumulator q of the leaf (eight lanes per leaf)
 #ifdef MM_KB_NOLEAF  // (ablation builds: timing only)
             if (l1 < 0)
@@ -218,29 +199,49 @@ __global__ void __launch_bounds__(KB_THREADS) kw_blocks_kernel(KbArgs a) {
                 const int off = loff[li] - c * KB_CHUNK, len = llen[li];
                 float res;
                 if (len < 8) {  // (a chunk shorter than 8: numpy's sequential sum)
-                    res = el[kb_pad(off)];
-                    for (int i = 1; i < len; ++i) res = __fadd_rn(res, el[kb_pad(off + i)]);
+                    res = el[word(off)];
+                    for (int i = 1; i < len; ++i) res = __fadd_rn(res, el[word(off + i)]);
                 } else {
+                    // this lane's frames off + q + 8g: word addresses advance by 8, and by
+                    // the tile padding TP - T when they cross into the next tile
+                    const int u0 = off + q + fb, t0 = u0 / T;
+                    int row = u0 - t0 * T, w = t0 * TP + row;
+                    auto next = [&]() __attribute__((always_inline)) {
+                        row += 8;
+                        w += 8;
+                        if (row >= T) {
+                            row -= T;
+                            w += TP - T;
+                        }
+                    };
                     float r;
                     const int full = len - (len & 7);
-                    if (full == 128 && (off & 127) == 0) {  // the common leaf: one padded run, reads issued at once
-                        const float *e = el + kb_pad(off) + q;
+                    if (full == 128) {  // the common leaf: every read issued at once
+                        int ad[16];
+#pragma unroll
+                        for (int g = 0; g < 16; ++g) {
+                            ad[g] = w;
+                            next();
+                        }
                         float v[16];
 #pragma unroll
-                        for (int g = 0; g < 16; ++g) v[g] = e[8 * g];
+                        for (int g = 0; g < 16; ++g) v[g] = el[ad[g]];
                         r = v[0];
 #pragma unroll
                         for (int g = 1; g < 16; ++g) r = __fadd_rn(r, v[g]);
-                    } else {  // (8-aligned groups never straddle a 128-frame run)
-                        r = el[kb_pad(off) + q];
-                        for (int i = 8; i < full; i += 8) r = __fadd_rn(r, el[kb_pad(off + i) + q]);
+                    } else {
+                        r = el[w];
+                        for (int i = 8; i < full; i += 8) {
+                            next();
+                            r = __fadd_rn(r, el[w]);
+                        }
                     }
                     // ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)): f32 addition commutes, so every
                     // lane of the eight ends with the same bits
                     r = __fadd_rn(r, __shfl_xor(r, 1));
                     r = __fadd_rn(r, __shfl_xor(r, 2));
                     res = __fadd_rn(r, __shfl_xor(r, 4));
-                    for (int i = full; i < len; ++i) res = __fadd_rn(res, el[kb_pad(off + i)]);
+                    for (int i = full; i < len; ++i) res = __fadd_rn(res, el[word(off + i)]);
                 }
                 if (q == 0) V[li] = res;
             }

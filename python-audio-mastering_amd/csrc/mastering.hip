@@ -1053,7 +1053,7 @@ static int kweight_exact(mm_ctx *c, const mm_job &j0, int64_t frames, int n_trk,
         kb.prog = c->kb_prog;
         kb.scale = (float)j0.block_scale;  // Python float * np.float32: the constant rounded to f32 (NEP 50)
         kb.zl = zl;
-        kb.stage_floats = kb_pad(KB_CHUNK);
+        kb.stage_floats = ((KB_CHUNK - 1) / Tt + 2) * TP;  // the padded tile runs a chunk can span
         kb.nvals = 2 * c->kb_nvals;  // (two value buffers)
         kb.pints = c->kb_pints;
         const size_t lds = (size_t)kb_lds_bytes(kb.stage_floats, kb.nvals, kb.pints);
