@@ -207,6 +207,19 @@ struct FinArgs {
     const double *gain_dev;  // device gain (loudness gated on the device) or null
     const short2 *mix;
     void *out;
+    // The chain's tail (its last finalize launch; ctl null otherwise): every block
+    // zeroes its slice of the control block past the readback area, and the last
+    // block to finish copies the readback area into the mapped host block, then
+    // zeroes it, so the next chain starts on a zeroed block with no fill or copy.
+    char *ctl;
+    int64_t ctl_bytes, rb_area;  // the control block, its readback area (both multiples of 4)
+    int rb_bytes;                // readback bytes copied out (a multiple of 4)
+    char *rb_host;               // device address of the mapped host block
+    unsigned *done;              // finished-block counters: FIN_DONE_LINES + 1, 128 B apart
 };
+// Blocks count themselves on FIN_DONE_LINES counters (block b on b % FIN_DONE_LINES),
+// the block completing a counter on one more: ONE device-scope atomic per block on
+// a shared address serialises (3.7 K blocks on C2: finalize 0.067 against 0.040 ms).
+constexpr int FIN_DONE_LINES = 64;
 
 }  // namespace mm

@@ -491,6 +491,7 @@ struct XoArgs {
     // frames n >= tail_from (the window's partial tile, look % T frames)
     double *E[3], *tail[3];
     int tail_from[3];
+    const double *zw;     // [T][8] zero-state weights (zs_weights; null: pass 1 runs the recurrence)
 };
 
 // this lane's channel's q^2; the lane pair's sums are added once per tile (exact
@@ -556,8 +557,15 @@ __device__ __forceinline__ void xo_pass(const XoArgs &a, int64_t g, int c, int l
 // multiply-adds (v_mad_i64_i32) of the pre-wrap quantiser output (+-32768 square
 // alike); the tail sums take the frames n >= tail_from through a select on the
 // uniform frame index.
-template <int CH, bool P2>
-__device__ __forceinline__ void xo_pass_full(const XoArgs &a, int64_t g0, int tid, double (&z)[4][2]) {
+// ZW (pass 1 of a block of whole tiles): the tile's zero-state end state as the
+// product of its T inputs with the stage's zero-state weights, z_d = sum_n W[n][d]
+// x_n (mastering.hip zs_weights): 8 independent FMAs per frame for the two
+// branches' 4 sections in place of the recurrence's chained sections, the weights
+// read from LDS (wl: the block's copy, broadcast reads; as scalar loads the
+// per-frame load latency was exposed: xover 0.150 against 0.126 ms).
+template <int CH, bool P2, bool ZW = false>
+__device__ __forceinline__ void xo_pass_full(const XoArgs &a, int64_t g0, int tid, double (&z)[4][2],
+                                             const double *wl = nullptr) {
     const double(*sos)[5] = a.sos;
     const int T = a.T;
     const int64_t G2 = a.G * 2;
@@ -571,6 +579,23 @@ __device__ __forceinline__ void xo_pass_full(const XoArgs &a, int64_t g0, int ti
         T, [&](int i) { return (qin0 + (int64_t)min(i, T - 1) * G2)[lo]; },
         [&](int16_t q) {
             const double x = (double)(int32_t)q * (1.0 / 32768.0);  // AME:199 int16 -> f32, exact
+            if constexpr (ZW && !P2) {
+                const double2 *w2 = reinterpret_cast<const double2 *>(wl + pn * 8);
+                double w[8];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const double2 v = w2[k];
+                    w[2 * k] = v.x;
+                    w[2 * k + 1] = v.y;
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    z[k][0] = fma(w[2 * k], x, z[k][0]);
+                    z[k][1] = fma(w[2 * k + 1], x, z[k][1]);
+                }
+                ++pn;
+                return;
+            }
             double yl = df2t<P2>(x, z[0][0], z[0][1], sos[0]);
             yl = df2t<P2>(yl, z[1][0], z[1][1], sos[1]);
             double yh = df2t<P2>(x, z[2][0], z[2][1], sos[2]);
@@ -626,8 +651,16 @@ __global__ void __launch_bounds__(LB_THREADS, 4) xover_kernel(XoArgs a, LbArgs l
     double zs[4][2] = {{0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}, {0.0, 0.0}};
     const int64_t g0 = (int64_t)blk * TPB;
     const bool full = (g0 + TPB) * a.T <= a.N_proc;  // block-uniform
-    if (full) xo_pass_full<CH, false>(a, g0, tid, zs);
-    else if (valid) xo_pass<CH, false>(a, g, c, len, zs);
+    if (full && a.zw) {  // the weights into LDS (the look-back scratch is free until lb_carry)
+        for (int i = tid; i < a.T * 8; i += LB_THREADS) smem[i] = a.zw[i];
+        __syncthreads();
+        xo_pass_full<CH, false, true>(a, g0, tid, zs, smem);
+        __syncthreads();  // (every wave has read the weights before lb_carry writes its scratch)
+    } else if (full) {
+        xo_pass_full<CH, false>(a, g0, tid, zs);
+    } else if (valid) {
+        xo_pass<CH, false>(a, g, c, len, zs);
+    }
     double z[8], s[8], rst[8];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {

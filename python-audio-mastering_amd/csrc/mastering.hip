@@ -62,6 +62,13 @@ struct mm_ctx {
     uint32_t comp_stamp = 0;  // stamp of the last queued fix-up sweep
     unsigned *comp_changed = nullptr;
     char *ctl = nullptr;                // the chain's control block (setup_control)
+    size_t ctl_bytes = 0, ctl_rba = 0;  // its size and readback area
+    // the block is zero from ctl_clean_ptr up to ctl_clean_bytes: the last chain's
+    // tail (finalize) zeroed it, so the next setup_control queues no fill
+    bool ctl_clean = false;
+    char *ctl_clean_ptr = nullptr;
+    size_t ctl_clean_bytes = 0;
+    bool tail_readback = false;         // the last queued finalize hands the readback area over
     uint32_t *ctl_claims = nullptr;     // its zeroed claim stamps
     int comp_iters = 0, comp_pending = 0;
     int comp_queue = 0;  // sweeps to queue with the next solve (0: COMP_SWEEPS; then the last solve's need + 1)
@@ -92,7 +99,7 @@ struct mm_ctx {
     uint32_t sat_code_m = 0;          // the code of k = -32768
     std::map<std::string, std::vector<double>> mats_cache;
     // pinned block the chain's results are copied into (one sync per chain)
-    char *rb = nullptr;
+    char *rb = nullptr, *rb_dev = nullptr;  // (rb_dev: its device address)
     size_t rb_cap = 0;
     // batch execution (mm_master_batch): child contexts, one stream each
     std::vector<mm_ctx *> children;
@@ -215,6 +222,61 @@ static int upload_tables(mm_ctx *c, const char *name, const mm_iir &f, LbArgs &l
     }
     lb.pw_tile = d;
     lb.pw_blk = d + MM_TILE_POW * 64;
+    return MM_OK;
+}
+
+// Zero-state weights of one stage over a whole tile of T frames (pass 1 of the
+// crossover as a product, XoArgs::zw): row n is the state after the tile from a
+// zero state with a unit input at frame n and zeros elsewhere, W[n] = A^(T-1-n) B
+// (A: one zero-input frame, B: the state one frame after a unit input), evaluated
+// in long double and rounded once.  Branch 0 is sections [0, nsec_branch0), branch 1
+// the rest, both fed by the stage input (csrc/lookback.h's layout).
+static void zs_weights(const mm_iir &f, int T, std::vector<double> &W) {
+    const int nsec = f.nsec, nb0 = f.nsec_branch0;
+    auto step = [&](const long double *z, long double x, long double *o) {
+        for (int br = 0; br < 2; ++br) {
+            long double u = x;
+            for (int s = br ? nb0 : 0; s < (br ? nsec : nb0); ++s) {
+                const double *c = f.sos[s];
+                const long double y = (long double)c[0] * u + z[2 * s];
+                o[2 * s] = (long double)c[1] * u - (long double)c[3] * y + z[2 * s + 1];
+                o[2 * s + 1] = (long double)c[2] * u - (long double)c[4] * y;
+                u = y;
+            }
+        }
+    };
+    W.assign((size_t)T * 8, 0.0);
+    long double v[8] = {0}, t[8] = {0}, zero[8] = {0};
+    step(zero, 1.0L, v);
+    for (int n = T - 1; n >= 0; --n) {
+        for (int d = 0; d < 2 * nsec; ++d) W[(size_t)n * 8 + d] = (double)v[d];
+        step(v, 0.0L, t);
+        for (int d = 0; d < 8; ++d) v[d] = t[d];
+    }
+}
+
+// The stage's zero-state weights on the device (rebuilt only when its sections or
+// the tile change); null with MM_ZS_RECUR (A/B: pass 1 as the recurrence).
+static int upload_zw(mm_ctx *c, const char *name, const mm_iir &f, int T, const double **out) {
+    static const bool recur = getenv("MM_ZS_RECUR") != nullptr;
+    *out = nullptr;
+    if (recur || f.nsec < 1 || f.nsec > 4) return MM_OK;
+    std::vector<double> key(f.sos[0], f.sos[0] + 20);
+    key.push_back((double)T);
+    key.push_back((double)f.nsec);
+    key.push_back((double)f.nsec_branch0);
+    const std::string kname = std::string("zw_") + name;
+    double *d;
+    RET(get_buf(c, kname.c_str(), (size_t)T * 8, &d));
+    std::vector<double> &cached = c->mats_cache[kname];
+    if (cached != key) {
+        std::vector<double> W;
+        zs_weights(f, T, W);
+        HIPCHK(c, hipMemcpyAsync(d, W.data(), W.size() * sizeof(double), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));  // host vector is transient
+        cached = key;
+    }
+    *out = d;
     return MM_OK;
 }
 
@@ -347,19 +409,42 @@ static int comp_back(mm_ctx *c) {
 // Pinned readback block of one chain pass (offsets in bytes): look-back error
 // word, sweep flags, re-walked frame count, loudness + gain, per-chunk active counts.
 constexpr size_t RB_ERR = 0, RB_FLAGS = 16, RB_WALKED = 80, RB_LG = 96, RB_TOTALS = 128;
+// finalize's done counters after the readback area (FIN_DONE_LINES lines of 128 B and
+// the top one; FinArgs::done)
+constexpr size_t FIN_DONE_BYTES = (size_t)(FIN_DONE_LINES + 1) * 128;
 static size_t rb_bytes(int64_t nch) { return RB_TOTALS + (size_t)12 * nch; }
+
+static int64_t comp_chunks(const mm_ctx *c) { return c->comp_on ? c->ca.GS / c->ca.SPC : 0; }
 
 static int ensure_rb(mm_ctx *c, size_t bytes) {
     if (c->rb_cap >= bytes) return MM_OK;
     if (c->rb) HIPCHK(c, hipHostFree(c->rb));
-    c->rb = nullptr;
+    c->rb = c->rb_dev = nullptr;
     c->rb_cap = 0;
-    HIPCHK(c, hipHostMalloc((void **)&c->rb, bytes, hipHostMallocDefault));
+    // mapped and coherent: the chain's last finalize block writes it directly
+    HIPCHK(c, hipHostMalloc((void **)&c->rb, bytes, hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(c, hipHostGetDevicePointer((void **)&c->rb_dev, c->rb, 0));
     c->rb_cap = bytes;
     return MM_OK;
 }
 
-static int64_t comp_chunks(const mm_ctx *c) { return c->comp_on ? c->ca.GS / c->ca.SPC : 0; }
+// Hand the readback area over in the chain's last finalize launch (FinArgs::ctl),
+// instead of a copy after it.
+static int attach_tail(mm_ctx *c, FinArgs &fa) {
+    static const bool off = getenv("MM_CTL_FILL") != nullptr;  // (A/B: the round-5 fill + copy)
+    c->tail_readback = false;
+    if (off || !c->ctl) return MM_OK;
+    const size_t rbb = rb_bytes(comp_chunks(c));
+    RET(ensure_rb(c, rbb + 64));
+    fa.ctl = c->ctl;
+    fa.ctl_bytes = (int64_t)c->ctl_bytes;
+    fa.rb_area = (int64_t)(c->ctl_rba + FIN_DONE_BYTES);
+    fa.rb_bytes = (int)rbb;
+    fa.rb_host = c->rb_dev;
+    fa.done = reinterpret_cast<unsigned *>(c->ctl + c->ctl_rba);
+    c->tail_readback = true;
+    return MM_OK;
+}
 
 // Queue the D2H copy of everything the host checks after the chain (no sync): the
 // readback area of the control block, in ONE copy.
@@ -428,6 +513,37 @@ static int evaluate_chain(mm_ctx *c, bool *converged) {
     return MM_OK;
 }
 
+// An extension after a tail hand-over starts from a zeroed control block: the
+// per-chunk active counts (comp_rms, once per chain) and the earlier passes'
+// re-walked counts are kept on the host and merged into the last readback.
+struct RbKeep {
+    bool on = false;
+    std::vector<int32_t> tot;
+    unsigned long long walked[2] = {0, 0};
+};
+static void rb_keep(mm_ctx *c, RbKeep &k) {
+    if (!c->tail_readback) return;  // (a copied readback: the device words accumulate)
+    const int32_t *tot = reinterpret_cast<const int32_t *>(c->rb + RB_TOTALS);
+    if (!k.on) k.tot.assign(tot, tot + 3 * comp_chunks(c));
+    const unsigned long long *w = reinterpret_cast<const unsigned long long *>(c->rb + RB_WALKED);
+    k.walked[0] += w[0];
+    k.walked[1] += w[1];
+    k.on = true;
+    c->comp_flags_fresh = true;  // the sweep flags are zero as well
+}
+// After the chain's last pass: merge what rb_keep held, and note a zeroed block.
+static void rb_finish(mm_ctx *c, const RbKeep &k) {
+    if (k.on) {
+        memcpy(c->rb + RB_TOTALS, k.tot.data(), k.tot.size() * sizeof(int32_t));
+        unsigned long long *w = reinterpret_cast<unsigned long long *>(c->rb + RB_WALKED);
+        w[0] += k.walked[0];
+        w[1] += k.walked[1];
+    }
+    c->ctl_clean = c->tail_readback;
+    c->ctl_clean_ptr = c->ctl;
+    c->ctl_clean_bytes = c->ctl_bytes;
+}
+
 static int chain_check(mm_ctx *c, bool *converged) {
     RET(queue_readback(c, false));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -458,25 +574,32 @@ static int solve_geometry(const mm_job *j, mm_solve_geom *g) {
     return g->chunk_plane_bytes < ((int64_t)1 << 31) ? MM_OK : MM_ERR_ARG;
 }
 
-// Control words of the whole chain, zeroed by ONE memset and read back by ONE
-// copy: the readback area (RB_* layout: look-back error word, sweep flags,
-// re-walked count, loudness + gain, per-chunk active counts), the sweeps' claim
-// stamps, then the eq / crossover / K-weighting look-back regions (each fresh
-// until its first use).
+// Control words of the whole chain: the readback area (RB_* layout: look-back
+// error word, sweep flags, re-walked count, loudness + gain, per-chunk active
+// counts), finalize's done counters, the sweeps' claim stamps, then the eq /
+// crossover / K-weighting look-back regions (each fresh until its first use).  The chain's
+// last finalize hands the readback area to the mapped host block and leaves the
+// whole block zeroed (FinArgs::ctl), so a chain after a completed one starts with
+// no fill and ends with no copy; otherwise ONE memset here and ONE copy at the end.
 static int setup_control(mm_ctx *c, unsigned nblk, int64_t nch, int64_t claims) {
     const size_t region = lb_flag_bytes(nblk);  // >= the K-weighting stage's (256 tiles per block)
     const size_t rba = (rb_bytes(nch) + 255) / 256 * 256, cla = ((size_t)claims * 4 + 255) / 256 * 256;
-    const size_t bytes = rba + cla + 3 * region;
+    const size_t bytes = rba + FIN_DONE_BYTES + cla + 3 * region;
     char *ctl;
     RET(get_buf(c, "ctl", bytes, &ctl));
-    HIPCHK(c, hipMemsetAsync(ctl, 0, bytes, c->stream));
+    static const bool always_fill = getenv("MM_CTL_FILL") != nullptr;  // (A/B: round 5's fill per chain)
+    if (always_fill || !c->ctl_clean || ctl != c->ctl_clean_ptr || bytes > c->ctl_clean_bytes)
+        HIPCHK(c, hipMemsetAsync(ctl, 0, bytes, c->stream));
+    c->ctl_clean = false;
     c->ctl = ctl;
+    c->ctl_bytes = bytes;
+    c->ctl_rba = rba;
     c->lb_error = reinterpret_cast<unsigned *>(ctl + RB_ERR);
     c->comp_changed = reinterpret_cast<unsigned *>(ctl + RB_FLAGS);
     c->gate_out = reinterpret_cast<double *>(ctl + RB_LG);
-    c->ctl_claims = reinterpret_cast<uint32_t *>(ctl + rba);
+    c->ctl_claims = reinterpret_cast<uint32_t *>(ctl + rba + FIN_DONE_BYTES);
     for (int r = 0; r < 3; ++r) {
-        c->ctl_lb[r] = reinterpret_cast<unsigned *>(ctl + rba + cla + r * region);
+        c->ctl_lb[r] = reinterpret_cast<unsigned *>(ctl + rba + FIN_DONE_BYTES + cla + r * region);
         c->ctl_fresh[r] = true;
     }
     c->comp_flags_fresh = true;
@@ -764,6 +887,8 @@ static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
         }
         LbArgs lb{};
         RET(upload_tables(c, "xover", j->xover, lb));
+        if ((size_t)T * 8 * sizeof(double) <= (size_t)lb_lds_bytes<8, 1>())  // (the weights alias its LDS)
+            RET(upload_zw(c, "xover", j->xover, T, &xa.zw));
         RET(lb_prepare(c, nblk, ch, lb, 1));
         if (ch == 2)
             RET(launch(c, "xover", xover_kernel<2>, dim3(nblk), dim3(LB_THREADS), lb_lds_bytes<8, 2>(), xa, lb,
@@ -1169,8 +1294,9 @@ extern "C" int mm_gate_loudness(const mm_job *j, const double *seg_energy, doubl
     return MM_OK;
 }
 
-static int finalize(mm_ctx *c, double gain, const double *gain_dev, int use_gain, void *d_out) {
+static int finalize(mm_ctx *c, double gain, const double *gain_dev, int use_gain, void *d_out, bool tail = false) {
     const mm_job *j = &c->job;
+    c->tail_readback = false;
     if (c->G == 0) return MM_OK;
     FinArgs fa{};
     fa.N_proc = j->frames_proc;
@@ -1185,6 +1311,7 @@ static int finalize(mm_ctx *c, double gain, const double *gain_dev, int use_gain
     fa.gain_dev = gain_dev;
     fa.mix = c->mix;
     fa.out = d_out;
+    if (tail) RET(attach_tail(c, fa));
     const size_t lds = (size_t)FIN_TILES * (j->tile + 1) * sizeof(short2);
     if (fa.ch == 2)
         return launch(c, "finalize", finalize_kernel<2>, dim3(blocks_for(c->G, FIN_TILES)), dim3(256), lds, fa);
@@ -1197,8 +1324,8 @@ static int finalize(mm_ctx *c, double gain, const double *gain_dev, int use_gain
 static int enqueue_tail(mm_ctx *c, const mm_job *j, void *d_out) {
     const bool lufs = j->lufs_on && c->G > 0;
     if (lufs) RET(kweight_device(c));
-    RET(finalize(c, 1.0, lufs ? c->gate_out + 1 : nullptr, j->lufs_on, d_out));
-    return queue_readback(c, lufs);
+    RET(finalize(c, 1.0, lufs ? c->gate_out + 1 : nullptr, j->lufs_on, d_out, true));
+    return c->tail_readback ? MM_OK : queue_readback(c, lufs);
 }
 
 static int enqueue_chain(mm_ctx *c, const mm_job *j, const void *d_in, void *d_out) {
@@ -1207,15 +1334,18 @@ static int enqueue_chain(mm_ctx *c, const mm_job *j, const void *d_in, void *d_o
 }
 
 static int complete_chain(mm_ctx *c, const mm_job *j, void *d_out, mm_result *res) {
+    RbKeep keep;
     for (;;) {
         HIPCHK(c, hipStreamSynchronize(c->stream));
         bool converged;
         RET(evaluate_chain(c, &converged));
         if (converged) break;
+        rb_keep(c, keep);
         RET(comp_sweeps(c, 8));
         RET(comp_back(c));
         RET(enqueue_tail(c, j, d_out));
     }
+    rb_finish(c, keep);
     if (res) {
         const bool lufs = j->lufs_on && c->G > 0;
         const double *lg = reinterpret_cast<const double *>(c->rb + RB_LG);
@@ -1439,6 +1569,7 @@ static int fused_finalize(mm_ctx *c, const mm_job *J, int n, const FusedPlan &p,
     const mm_job &j0 = J[0];
     const int T = j0.tile;
     const size_t lds = (size_t)FIN_TILES * (T + 1) * sizeof(short2);
+    c->tail_readback = false;
     for (int i = 0; i < n; ++i) {
         FinArgs fa{};
         fa.N_proc = J[i].frames_proc;
@@ -1453,6 +1584,7 @@ static int fused_finalize(mm_ctx *c, const mm_job *J, int n, const FusedPlan &p,
         fa.gain_dev = j0.lufs_on ? lg + 2 * i + 1 : nullptr;
         fa.mix = c->mix;
         fa.out = d_out[i];
+        if (i == n - 1 && fa.G > 0) RET(attach_tail(c, fa));
         const dim3 grid(blocks_for(fa.G, FIN_TILES));
         if (fa.ch == 2) RET(launch(c, "finalize", finalize_kernel<2>, grid, dim3(256), lds, fa));
         else RET(launch(c, "finalize", finalize_kernel<1>, grid, dim3(256), lds, fa));
@@ -1493,7 +1625,7 @@ static int fused_enqueue(mm_ctx *c, int n, const mm_job *J, const void *const *d
     RET(get_buf(c, "fz_lg", (size_t)2 * n, &lg));
     if (lufs) RET(fused_loudness(c, j0, n, p, lg));
     RET(fused_finalize(c, J, n, p, lg, d_out));
-    return queue_readback(c, lufs);
+    return c->tail_readback ? MM_OK : queue_readback(c, lufs);
 }
 
 static int fused_complete(mm_ctx *c, int n, const mm_job *J, void *const *d_out, mm_result *res, const FusedPlan &p) {
@@ -1501,17 +1633,20 @@ static int fused_complete(mm_ctx *c, int n, const mm_job *J, void *const *d_out,
     const bool lufs = j0.lufs_on != 0;
     double *lg;
     RET(get_buf(c, "fz_lg", (size_t)2 * n, &lg));
+    RbKeep keep;
     for (;;) {
         HIPCHK(c, hipStreamSynchronize(c->stream));
         bool converged;
         RET(evaluate_chain(c, &converged));
         if (converged) break;
+        rb_keep(c, keep);
         RET(comp_sweeps(c, 8));
         RET(comp_back(c));
         if (lufs) RET(fused_loudness(c, j0, n, p, lg));
         RET(fused_finalize(c, J, n, p, lg, d_out));
-        RET(queue_readback(c, lufs));
+        if (!c->tail_readback) RET(queue_readback(c, lufs));
     }
+    rb_finish(c, keep);
     if (!res) return MM_OK;
     std::vector<double> l2((size_t)2 * n, 0.0);
     if (lufs) HIPCHK(c, hipMemcpy(l2.data(), lg, l2.size() * sizeof(double), hipMemcpyDeviceToHost));

@@ -222,6 +222,11 @@ def test_compressor_resume_path(oracle, monkeypatch, warmup):
     assert info["comp_iters"] >= 1, info["comp_iters"]  # the one queued sweep changed ends
     ref, L = oracle.master(pcm, 44100, P_HOT, return_loudness=True)
     _check(out, info, ref, L)
+    # the control block is zeroed by each pass's finalize: the resumed chain still
+    # reports the first pass's active band-frames (kept on the host)
+    monkeypatch.delenv("MM_COMP_SWEEPS")
+    _, info2 = master_pcm(pcm, 44100, P_HOT)
+    assert info["comp_active"] == info2["comp_active"] > 0, (info["comp_active"], info2["comp_active"])
 
 
 @pytest.mark.parametrize("channels,params,in_i16,rate", [(2, P_FULL, False, 44100), (1, P_HOT, True, 44100),
