@@ -165,8 +165,8 @@ int mm_sync(mm_ctx *ctx);
    mm_solve_geometry (round 4); 3 = mm_solve_geom.walk_block, the device loudness
    path in composable steps with a world check and the applied gain returned,
    device-pointer collectives (round 5); 4 = mm_job.sat_table / sat_key,
-   mm_op_saturation_table, mm_np_sum_f32, mm_solve_geom.col_block / rms_group_tiles
-   (round 6).  A caller built against an older header must
+   mm_op_saturation_table, mm_np_sum_f32, mm_check_compressor_math,
+   mm_solve_geom.col_block / rms_group_tiles (round 6).  A caller built against an older header must
    refuse a library whose version differs from its own MM_ABI_VERSION. */
 #define MM_ABI_VERSION 4
 int mm_version(void);
@@ -250,6 +250,12 @@ int mm_gate_loudness(const mm_job *job, const double *seg_energy, double *loudne
  * chunks, pairwise leaves of <= 128 with eight accumulators): a CPU check that the
  * device sums in numpy's order. */
 int mm_np_sum_f32(const float *x, int64_t n, float *out);
+/* Verification entry (no reference counterpart): the compressor's device exp10 and
+ * exact rms on host arrays of n arguments.  what 0: out[i] = exp10_tab(a[i]) (the
+ * gain 10^y of comp_apply, y in [-3, 0]); what 1: out[i] = rms_exact1(a[i], b[i])
+ * (comp_rms's audioop.rms: isqrt(floor(S / n)) for integer S = a[i] < 2^53 and
+ * n = b[i] >= 1).  Checked by tests/test_compressor_math.py. */
+int mm_check_compressor_math(mm_ctx *ctx, int what, const double *a, const double *b, int64_t n, double *out);
 /* Apply gain + soft limiter + quantise (AME:84-89) to the staged mix. */
 int mm_finalize(mm_ctx *ctx, double gain_linear, int use_gain, void *d_out);
 /* Copy the staged pre-gain int16 mix (interleaved) to host (parity probe). */

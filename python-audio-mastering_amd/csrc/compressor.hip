@@ -1279,6 +1279,21 @@ __device__ __forceinline__ double exp10_tab(double y, const double2 *tab) {
     return ldexp(fma(t.x, p, t.y * p), k >> 6);
 }
 
+// Verification of the compressor's two hand-made elementary functions on the
+// device (mm_check_compressor_math, tests/test_compressor_math.py): what 0: out =
+// exp10_tab(a) (10^a); what 1: out = rms_exact1(a, b) with comp_rms's biased
+// reciprocal (isqrt(floor(a / b)) for integers a < 2^53, b >= 1).
+__global__ void __launch_bounds__(256) comp_math_kernel(int what, const double *xa, const double *xb, int64_t n,
+                                                       double *out) {
+    __shared__ double2 etab[64];
+    if (threadIdx.x < 64) etab[threadIdx.x] = EXP2_TAB64[threadIdx.x];
+    __syncthreads();
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    if (what == 0) out[i] = exp10_tab(xa[i], etab);
+    else out[i] = (double)rms_exact1(xa[i], xb[i], rcp_biased(xb[i]));
+}
+
 #ifndef MM_APPLY_MINB
 #define MM_APPLY_MINB 1
 #endif

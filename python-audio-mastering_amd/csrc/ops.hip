@@ -446,6 +446,24 @@ int mm_op_saturation_table(mm_ctx *c, int dtype, const void *in, int64_t n, doub
     return PW_DISPATCH(PW_SAT, dtype, in, bytes, out, bytes, pa);
 }
 
+int mm_check_compressor_math(mm_ctx *c, int what, const double *a, const double *b, int64_t n, double *out) {
+    if (!c || n < 0 || (what != 0 && what != 1) || (n > 0 && (!a || !out || (what == 1 && !b))))
+        return set_err(c, MM_ERR_ARG, "bad arguments");
+    if (n == 0) return MM_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    double *da, *db, *dout;
+    RET(get_buf(c, "cm_a", (size_t)n, &da));
+    RET(get_buf(c, "cm_b", (size_t)n, &db));
+    RET(get_buf(c, "cm_out", (size_t)n, &dout));
+    HIPCHK(c, hipMemcpyAsync(da, a, (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
+    if (what == 1) HIPCHK(c, hipMemcpyAsync(db, b, (size_t)n * 8, hipMemcpyHostToDevice, c->stream));
+    RET(launch(c, "comp_math", comp_math_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, what, (const double *)da,
+               (const double *)db, n, dout));
+    HIPCHK(c, hipMemcpyAsync(out, dout, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return MM_OK;
+}
+
 int mm_op_saturation(mm_ctx *c, int dtype, const void *in, int64_t n, double percent, void *out) {
     return mm_op_saturation_table(c, dtype, in, n, percent, nullptr, out);
 }

@@ -88,7 +88,7 @@ EXPORTS = ("mm_create", "mm_destroy", "mm_last_error", "mm_sync", "mm_version", 
            "mm_op_pcm_to_float", "mm_op_saturation", "mm_op_saturation_table", "mm_op_stereo_width", "mm_op_quantize", "mm_op_soft_limiter",
            "mm_op_gain", "mm_op_sosfilt", "mm_op_loudness", "mm_op_multiband", "mm_master_batch",
            "mm_op_saturation_legacy", "mm_op_soft_limiter_legacy", "mm_op_sosfilt_mix", "mm_op_compress_bands",
-           "mm_solve_geometry", "mm_np_sum_f32")
+           "mm_solve_geometry", "mm_np_sum_f32", "mm_check_compressor_math")
 
 _lib = None
 _lock = threading.Lock()
@@ -164,6 +164,8 @@ def load():
             "mm_op_compress_bands": ([vp, P(MMJob), vp, vp, vp, vp], ctypes.c_int),
             "mm_solve_geometry": ([P(MMJob), P(MMSolveGeom)], ctypes.c_int),
             "mm_np_sum_f32": ([P(ctypes.c_float), ctypes.c_int64, P(ctypes.c_float)], ctypes.c_int),
+            "mm_check_compressor_math": ([vp, ctypes.c_int, c_double_p, c_double_p, ctypes.c_int64, c_double_p],
+                                         ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             fn = getattr(lib, name)
