@@ -132,12 +132,11 @@ struct SatArgs {
     float keep, mix, drive;
     int on;
     const float *tab;  // [65536] the reference's apply_saturation on the int16 grid (mm_job.sat_table), or null
-    // [2048] 2-bit codes per |k| <= 32767 (16 per word): numpy's value minus the
-    // device's tanhf evaluation, as float bit patterns: 0 equal, 1 +1, 2 -1; built on
+    // [4096] signed 2-bit codes per grid index k + 32768 (16 per word): numpy's value
+    // minus the device's tanhf evaluation, as float bit patterns (0, +1, -1); built on
     // the device from tab (sat_corr_kernel) and used only when complete (no entry off
     // by more than one step), else null (tab alone: a gather per sample)
     const uint32_t *corr;
-    uint32_t code_m;  // the code of k = -32768
 };
 
 // apply_saturation's value for x = k / 32768 from the host table (numpy's float32

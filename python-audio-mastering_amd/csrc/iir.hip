@@ -68,24 +68,24 @@ __device__ __forceinline__ float saturate_dev(float x, const SatArgs &s) {
 #endif
     return __fadd_rn(__fmul_rn(s.keep, x), __fmul_rn(s.mix, t));
 }
-// With the correction codes: the device value, then the 2-bit code of its grid
-// entry moves it onto numpy's bits; the rare entries more than one step apart read
-// the full table.  The codes are one table for |k| (both the device's and numpy's
-// values are odd in x; sat_corr_kernel marks an entry 3 where the two signs
-// disagree): 2049 words, 8 KB (the EQ kernel gathers them at staging).  Without them
+// With the correction codes: the device value, then the signed 2-bit code of its
+// grid entry (numpy minus device as float bit patterns: 0, +1, -1) moves it onto
+// numpy's bits.  One code per grid index i = k + 32768 (16 per word, 16 KB, in the
+// EQ kernel's LDS): one unsigned range check, one LDS word, one signed bit-field
+// extract (round 6's first version folded |k| into an 8 KB table: 5 more VALU per
+// sample).  The codes are only used when every entry is within one step
+// (sat_corr_kernel's exception count, checked on the host once per table): then the
+// exciter issues no global load in the EQ's per-frame loop (a conditional one there
+// made the compiler drain the staging prefetch at every frame).  Without them
 // (pointwise operators): the full table's entry, a gather per sample.
-// The codes are only used when no entry is 3 (sat_corr_kernel's exception flag,
-// checked on the host once per table): then the exciter issues no global load in
-// the EQ's per-frame loop (a conditional one there made the compiler drain the
-// staging prefetch at every frame).
 __device__ __forceinline__ float saturate_corr(float x, const SatArgs &s, const uint32_t *corr) {
     float y = saturate_dev(x, s);
     const float sc = x * 32768.0f;  // exact
     const int k = (int)sc;
-    if ((float)k == sc && k >= -32768 && k <= 32767) {
-        const unsigned u = (unsigned)abs(k);
-        const unsigned code = k == -32768 ? s.code_m : (corr[u >> 4] >> ((u & 15u) * 2u)) & 3u;
-        y = __int_as_float(__float_as_int(y) + (int)(code & 1u) - (int)(code >> 1));
+    const unsigned i = (unsigned)(k + 32768);
+    if ((float)k == sc && i < 65536u) {
+        const int d = __builtin_amdgcn_sbfe((int)corr[i >> 4], (i & 15u) * 2u, 2u);
+        y = __int_as_float(__float_as_int(y) + d);
     }
     return y;
 }
@@ -96,31 +96,22 @@ __device__ __forceinline__ float saturate(float x, const SatArgs &s) {
     return saturate_dev(x, s);
 }
 
-constexpr int SAT_CORR_WORDS = 2048;  // |k| = 0 .. 32767, 16 codes per word (8 KB)
-// Builds SatArgs::corr from SatArgs::tab: thread w packs |k| = 16w .. 16w + 15;
-// exceptions[0] counts entries that need the table, exceptions[1] = k = -32768's code.
+constexpr int SAT_CORR_WORDS = 4096;  // i = k + 32768 = 0 .. 65535, 16 codes per word (16 KB)
+// Builds SatArgs::corr from SatArgs::tab: thread w packs i = 16w .. 16w + 15 as signed
+// 2-bit fields; exceptions[0] counts entries more than one step apart (their field
+// is 0 and the codes are not used).
 __global__ void __launch_bounds__(256) sat_corr_kernel(SatArgs s, uint32_t *corr, unsigned *exceptions) {
     const int w = blockIdx.x * 256 + threadIdx.x;
     if (w >= SAT_CORR_WORDS) return;
-    auto code_of = [&](int k) {
-        const float x = (float)k * (1.0f / 32768.0f);
-        const int d = __float_as_int(s.tab[k + 32768]) - __float_as_int(saturate_dev(x, s));
-        return d == 0 ? 0u : d == 1 ? 1u : d == -1 ? 2u : 3u;
-    };
     uint32_t word = 0;
     for (int e = 0; e < 16; ++e) {
-        const int u = w * 16 + e;
-        const uint32_t cp = code_of(u), cn = code_of(-u);
-        const uint32_t code = cp == cn ? cp : 3u;
-        word |= code << (2 * e);
-        if (code == 3u) atomicAdd(exceptions, 1u);
+        const int i = w * 16 + e, k = i - 32768;
+        const float x = (float)k * (1.0f / 32768.0f);
+        const int d = __float_as_int(s.tab[i]) - __float_as_int(saturate_dev(x, s));
+        if (d < -1 || d > 1) atomicAdd(exceptions, 1u);
+        else word |= ((uint32_t)d & 3u) << (2 * e);
     }
     corr[w] = word;
-    if (w == 0) {
-        const uint32_t cm = code_of(-32768);
-        exceptions[1] = cm;
-        if (cm == 3u) atomicAdd(exceptions, 1u);
-    }
 }
 
 // The exciter as a pointwise pre-pass (decoded input -> f32), for the EQ kernel when
@@ -212,9 +203,10 @@ struct EqArgs {
 
 // Staging buffer: two steps of EQ_STAGE frames for the block's TPB tiles (rows
 // padded by one frame against bank conflicts); the look-back scratch aliases it
-// between the passes.  The exciter's codes are a static 8 KB beside it (three
-// blocks per CU; an unpadded XOR-swizzled stage with the codes in its place, four
-// blocks per CU, measured slower: eq 0.234 against 0.173 ms).
+// between the passes.  The exciter's codes are a static 16 KB beside it (51 KB per
+// block: three blocks per CU, as with round 6's first 8 KB table; an unpadded
+// XOR-swizzled stage with the codes in its place, four blocks per CU, measured
+// slower: eq 0.234 against 0.173 ms).
 template <int CH>
 constexpr int eq_stage_bytes() {
     return 2 * (LB_THREADS / CH) * (EQ_STAGE + 1) * CH * (int)sizeof(float);

@@ -96,7 +96,6 @@ struct mm_ctx {
     uint64_t lut_key[3] = {0, 0, 0};  // content keys of the band tables on the device (0: none)
     uint64_t sat_key = 0;             // content key of the exciter table on the device (0: none)
     bool sat_codes = false;           // its correction codes are complete (no entry needs the table)
-    uint32_t sat_code_m = 0;          // the code of k = -32768
     std::map<std::string, std::vector<double>> mats_cache;
     // pinned block the chain's results are copied into (one sync per chain)
     char *rb = nullptr, *rb_dev = nullptr;  // (rb_dev: its device address)
@@ -814,20 +813,18 @@ static int stage_front(mm_ctx *c, const mm_job *j, const void *d_in) {
         ea.sat.tab = tab;
         if (j->sat_key == 0 || c->sat_key != j->sat_key) {  // once per table: build the codes, count exceptions
             unsigned *exc;
-            RET(get_buf(c, "sat_exc", 2, &exc));
+            RET(get_buf(c, "sat_exc", 1, &exc));
             HIPCHK(c, hipMemcpyAsync(tab, j->sat_table, 65536 * sizeof(float), hipMemcpyHostToDevice, c->stream));
-            HIPCHK(c, hipMemsetAsync(exc, 0, 2 * sizeof(unsigned), c->stream));
+            HIPCHK(c, hipMemsetAsync(exc, 0, sizeof(unsigned), c->stream));
             RET(launch(c, "sat_corr", sat_corr_kernel, dim3((SAT_CORR_WORDS + 255) / 256), dim3(256), 0, ea.sat, corr,
                        exc));
-            unsigned e2[2] = {1, 0};
-            HIPCHK(c, hipMemcpyAsync(e2, exc, 2 * sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
+            unsigned e1 = 1;
+            HIPCHK(c, hipMemcpyAsync(&e1, exc, sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
             HIPCHK(c, hipStreamSynchronize(c->stream));
-            c->sat_codes = e2[0] == 0;
-            c->sat_code_m = e2[1];
+            c->sat_codes = e1 == 0;
             c->sat_key = j->sat_key;
         }
         // codes when complete (else, and for A/B: a full-table gather per sample)
-        ea.sat.code_m = c->sat_code_m;
         if (c->sat_codes && !getenv("MM_SAT_GATHER")) ea.sat.corr = corr;
         if (getenv("MM_SAT_TANHF")) ea.sat.tab = nullptr, ea.sat.corr = nullptr;  // (A/B: round 5's tanhf alone)
         if (ea.sat.tab && !ea.sat.corr && j->eq.nsec > 0 && N > 0) {
