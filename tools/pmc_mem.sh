@@ -13,6 +13,7 @@ run() {
     python3 bench.py --workload $wl $extra --steps 3 --warmup 2 --profile-steps 1 --no-cpu-baseline \
     > $out/$name.log 2>&1
   local rc=$?; echo "$name rc=$rc"; [ $rc -ne 0 ] && { tail -5 $out/$name.log; exit $rc; }
+  return 0
 }
 run ta1 --pmc TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum
 run ta2 --pmc TA_DATA_STALLED_BY_TC_CYCLES_sum TA_TOTAL_WAVEFRONTS_sum
