@@ -310,7 +310,11 @@ def test_sweep_queue_across_settings_on_one_context():
     longer track: the sweep count a context learns from its last solve is reset
     when the compressor settings or the geometry change (comp_signature), and the
     output never depends on the context's history (the solve is exact for any
-    number of queued sweeps): every job equals the same job on a fresh context."""
+    number of queued sweeps): every job equals the same job on a fresh context.
+    The jobs also exercise the control block's hand-over (round 6): each chain's last
+    finalize block zeroes the block for the next one, whose fill is then skipped when
+    it needs no more bytes (the 40 s jobs after the 70 s one), and the readback it
+    hands over (loudness, active and re-walked counts) matches a fresh context's."""
     import ctypes
 
     from mastering_amd import Job, native
@@ -339,6 +343,8 @@ def test_sweep_queue_across_settings_on_one_context():
         assert np.array_equal(out, ref)
         assert res.loudness == rres.loudness
         assert res.comp_iters == rres.comp_iters
+        assert (res.comp_active, res.comp_walked, res.comp_jumped) == (rres.comp_active, rres.comp_walked,
+                                                                      rres.comp_jumped)
     shared.close()
 
 
