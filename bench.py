@@ -615,7 +615,11 @@ def main(argv=None):
                          "valu_ceiling": valu, "valu": vfloor},
             "chain": {"device_ms_per_step": sum(v[0] for v in per.values()),
                       "comp_iters": iters, "comp_active_frames": active, "comp_rewalked_frames": walked, "comp_jumped_frames": jumped,
-                      "kernels_ms_per_step": {k: round(v[0], 4) for k, v in per.items()}},
+                      "kernels_ms_per_step": {k: round(v[0], 4) for k, v in per.items()},
+                      # launches per step (library kernels; comp_fix counts every queued sweep,
+                      # quiet ones included; runtime copies / fills are not library launches)
+                      "launches_per_step": round(sum(v[1] for v in per.values()), 2),
+                      "kernel_launches_per_step": {k: round(v[1], 2) for k, v in per.items()}},
         }
         if args.workload == "C4":
             line["chain"]["loudness"] = res[0]["loudness"] if res else None
